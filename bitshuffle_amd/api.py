@@ -1,0 +1,209 @@
+"""numpy / torch front end over the C-ABI.
+
+Host functions mirror bitshuffle/ext.pyx of the reference one for one
+(argument names, C-contiguity check, `out=` reuse, RuntimeError("Failed.
+Error code %d.", code) on negative returns, and decompress_lz4's check that
+the whole input buffer was consumed, ext.pyx:501-504).  Unlike the Cython
+wrapper, sizes are 64-bit, so arrays beyond 2**31 elements work.
+
+Device functions take torch tensors that live on a HIP device and enqueue on
+the current torch stream (or `stream=`); nothing is copied to the host except
+the compressed length when `sync=True`.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import BshufError, lib
+
+
+def _fail(code, what="Failed. Error code %d."):
+    raise BshufError(what % code, int(code))
+
+
+def _check(code):
+    if code < 0:
+        _fail(code)
+    return code
+
+
+def _make_array(shape, dtype, out=None):
+    # bitshuffle/ext.pyx:124-133
+    if out is None:
+        return np.empty(shape, dtype=dtype)
+    size = int(np.prod(shape))
+    base = out if out.base is None else out.base
+    return base.ravel().view(dtype)[:size].reshape(shape)
+
+
+def _setup_arr(arr, out=None):
+    # bitshuffle/ext.pyx:136-145
+    if not arr.flags["C_CONTIGUOUS"]:
+        raise ValueError("Input array must be C-contiguous.")
+    return _make_array(tuple(arr.shape), arr.dtype, out), arr.size, arr.dtype.itemsize
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def default_block_size(elem_size):
+    return int(lib.bshuf_default_block_size(elem_size))
+
+
+def compress_lz4_bound(size, elem_size, block_size=0):
+    return int(lib.bshuf_compress_lz4_bound(size, elem_size, block_size))
+
+
+# ---------------------------------------------------------------- host API
+def bitshuffle(arr, block_size=0, out=None):
+    """Bitshuffle an array (reference bitshuffle/ext.pyx:311-353)."""
+    out, size, itemsize = _setup_arr(arr, out)
+    _check(lib.bshuf_bitshuffle(_ptr(arr), _ptr(out), size, itemsize, block_size))
+    return out
+
+
+def bitunshuffle(arr, block_size=0, out=None):
+    """Undo bitshuffle (reference bitshuffle/ext.pyx:356-398)."""
+    out, size, itemsize = _setup_arr(arr, out)
+    _check(lib.bshuf_bitunshuffle(_ptr(arr), _ptr(out), size, itemsize, block_size))
+    return out
+
+
+def compress_lz4(arr, block_size=0, out=None):
+    """Bitshuffle then LZ4-compress; returns the framed uint8 stream
+    (reference bitshuffle/ext.pyx:401-447)."""
+    if not arr.flags["C_CONTIGUOUS"]:
+        raise ValueError("Input array must be C-contiguous.")
+    size, itemsize = arr.size, arr.dtype.itemsize
+    bound = compress_lz4_bound(size, itemsize, block_size)
+    if bound > (1 << 62):  # the (size_t)-81 quirk of an invalid block size
+        _fail(-81)
+    out = _make_array((max(bound, 1),), np.uint8, out)
+    count = _check(lib.bshuf_compress_lz4(_ptr(arr), _ptr(out), size, itemsize, block_size))
+    return out[:count]
+
+
+def decompress_lz4(arr, shape, dtype, block_size=0, out=None):
+    """LZ4-decompress then bitunshuffle (reference bitshuffle/ext.pyx:452-505)."""
+    if not arr.flags["C_CONTIGUOUS"]:
+        raise ValueError("Input array must be C-contiguous.")
+    dtype = np.dtype(dtype)
+    size = int(np.prod(shape))
+    out = _make_array(tuple(shape), dtype, out)
+    count = _check(lib.bshuf_decompress_lz4(_ptr(arr), _ptr(out), size, dtype.itemsize,
+                                            block_size))
+    if count != arr.size:
+        msg = "Decompressed different number of bytes than input buffer size."
+        msg += "Input buffer %d, decompressed %d." % (arr.size, count)
+        raise BshufError(msg, count)
+    return out
+
+
+# -------------------------------------------------------------- device API
+def _torch():
+    import torch
+    return torch
+
+
+def _stream(stream):
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+
+def _dptr(t):
+    if not t.is_cuda:
+        raise ValueError("device functions need a HIP (torch 'cuda') tensor")
+    if not t.is_contiguous():
+        raise ValueError("Input array must be C-contiguous.")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def bitshuffle_dev(t, block_size=0, out=None, stream=None):
+    out = _torch().empty_like(t) if out is None else out
+    _check(lib.bshuf_bitshuffle_dev(_dptr(t), _dptr(out), t.numel(), t.element_size(),
+                                    block_size, _stream(stream)))
+    return out
+
+
+def bitunshuffle_dev(t, block_size=0, out=None, stream=None):
+    out = _torch().empty_like(t) if out is None else out
+    _check(lib.bshuf_bitunshuffle_dev(_dptr(t), _dptr(out), t.numel(), t.element_size(),
+                                      block_size, _stream(stream)))
+    return out
+
+
+def compress_lz4_workspace(numel, elem_size, block_size=0, device=None):
+    torch = _torch()
+    n = int(lib.bshuf_compress_lz4_dev_workspace(numel, elem_size, block_size))
+    return torch.empty(max(n, 256), dtype=torch.uint8, device=device or "cuda")
+
+
+def decompress_lz4_workspace(in_nbytes, numel, elem_size, block_size=0, device=None):
+    torch = _torch()
+    n = int(lib.bshuf_decompress_lz4_dev_workspace(in_nbytes, numel, elem_size, block_size))
+    return torch.empty(max(n, 256), dtype=torch.uint8, device=device or "cuda")
+
+
+def compress_lz4_dev(t, block_size=0, out=None, workspace=None, result=None, offsets=None,
+                     stream=None, sync=True):
+    """Device-resident bshuf_compress_lz4.  Returns the framed stream as a uint8
+    tensor view (sync=True), or (out, result) where result is a 1-element int64
+    device tensor holding the byte count / error (sync=False)."""
+    torch = _torch()
+    n, es = t.numel(), t.element_size()
+    bound = compress_lz4_bound(n, es, block_size)
+    if bound > (1 << 62):
+        _fail(-81)
+    if out is None:
+        out = torch.empty(max(bound, 1), dtype=torch.uint8, device=t.device)
+    if result is None:
+        result = torch.empty(1, dtype=torch.int64, device=t.device)
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    wsb = workspace.numel() if workspace is not None else 0
+    offp = _dptr(offsets) if offsets is not None else None
+    _check(lib.bshuf_compress_lz4_dev(_dptr(t), _dptr(out), n, es, block_size, ws, wsb,
+                                      _dptr(result), offp, _stream(stream)))
+    if not sync:
+        return out, result
+    count = int(result.item())
+    if count < 0:
+        _fail(count)
+    return out[:count]
+
+
+def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None, result=None,
+                       offsets=None, stream=None, sync=True):
+    """Device-resident bshuf_decompress_lz4 of the whole uint8 tensor `buf`
+    (its length is the exact stream length)."""
+    torch = _torch()
+    size = 1
+    for s in shape:
+        size *= int(s)
+    if out is None:
+        out = torch.empty(tuple(shape), dtype=dtype, device=buf.device)
+    if result is None:
+        result = torch.empty(1, dtype=torch.int64, device=buf.device)
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    wsb = workspace.numel() if workspace is not None else 0
+    offp = _dptr(offsets) if offsets is not None else None
+    _check(lib.bshuf_decompress_lz4_dev(_dptr(buf), buf.numel(), _dptr(out), size,
+                                        out.element_size(), block_size, ws, wsb, _dptr(result),
+                                        offp, _stream(stream)))
+    if not sync:
+        return out, result
+    count = int(result.item())
+    if count < 0:
+        _fail(count)
+    if count != buf.numel():
+        raise BshufError("Decompressed different number of bytes than input buffer size."
+                         "Input buffer %d, decompressed %d." % (buf.numel(), count), count)
+    return out
+
+
+def synth_fill_dev(t, gen, first=0, seed=12345, stream=None):
+    """Fill tensor t with synthetic input G0 (int32 ramp), G1 (int16) or G2 (float32)."""
+    _check(lib.bshuf_synth_fill_dev(_dptr(t), t.numel(), gen, first, seed, _stream(stream)))
+    return t

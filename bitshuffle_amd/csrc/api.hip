@@ -1,0 +1,385 @@
+// api.hip -- the drop-in C-ABI (include/bitshuffle.h, include/bitshuffle_core.h).
+//
+// Host-pointer entry points keep the reference's contract exactly
+// (src/bitshuffle_core.c:2038-2062, src/bitshuffle.c:214-247): they stage the
+// buffers through device memory on a per-thread HIP stream and run the gfx950
+// kernels.  There is no CPU compute path: without a usable HIP device every
+// entry point returns -70.  The *_dev entry points take device pointers and
+// only enqueue work.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/bitshuffle.h"
+#include "launch.h"
+
+using namespace bshuf;
+
+namespace {
+
+constexpr int64_t kErrHip = -70;
+constexpr int64_t kErrUnsupported = -71;
+
+struct Plan {
+    Layout L;
+    int64_t tail;  // raw tail bytes
+    int64_t nb;    // nblocks
+};
+
+// Blocking of src/bitshuffle_core.c:1877-1931.
+int64_t make_plan(size_t size, size_t elem_size, size_t block_size, Plan& p) {
+    if (elem_size == 0) return kErrUnsupported;
+    if (block_size == 0) block_size = bshuf_default_block_size(elem_size);
+    if (block_size % kBlockedMult) return -81;
+    if (block_size * elem_size > (size_t)INT32_MAX / 2 || elem_size > 65536) return kErrUnsupported;
+    p.L.bs = (int32_t)block_size;
+    p.L.E = (int32_t)elem_size;
+    p.L.nfull = (int64_t)(size / block_size);
+    size_t last = size % block_size;
+    last -= last % kBlockedMult;
+    p.L.last = (int32_t)last;
+    p.tail = (int64_t)((size % kBlockedMult) * elem_size);
+    p.nb = p.L.nblocks();
+    return 0;
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Carver {
+    uint8_t* base;
+    size_t off = 0;
+    template <class T>
+    T* take(size_t bytes) {
+        T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+        off += al256(bytes);
+        return p;
+    }
+};
+
+bool have_device() {
+    static int n = -1;
+    if (n < 0) {
+        int c = 0;
+        n = (hipGetDeviceCount(&c) == hipSuccess) ? c : 0;
+    }
+    return n > 0;
+}
+
+hipStream_t thread_stream() {
+    thread_local hipStream_t s = nullptr;
+    if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    return s;
+}
+
+// ---- workspace layouts -------------------------------------------------------
+size_t enc_ws(const Plan& p, EncodeBufs* b, uint8_t* base) {
+    Carver c{base};
+    const int64_t slot = encode_slot_bytes(p.L);
+    EncodeBufs x;
+    x.slot = slot;
+    x.scratch = c.take<uint8_t>((size_t)(p.nb * slot));
+    x.foot = c.take<uint64_t>((size_t)(p.nb + 1) * 8);
+    x.offs = c.take<uint64_t>((size_t)(p.nb + 1) * 8);
+    x.scan_tmp_bytes = encode_scan_tmp_bytes(p.nb);
+    x.scan_tmp = c.take<void>(x.scan_tmp_bytes);
+    if (b) *b = x;
+    return c.off;
+}
+
+size_t dec_ws(const Plan& p, int64_t blocks_end, bool need_index, DecodeBufs* b, uint8_t* base) {
+    Carver c{base};
+    DecodeBufs x;
+    x.chunk = index_chunk_bytes(p.L);
+    x.nchunks = blocks_end > 0 ? (blocks_end + x.chunk - 1) / x.chunk : 0;
+    x.offs = c.take<uint64_t>((size_t)p.nb * 8 + 8);
+    x.status = c.take<int64_t>((size_t)p.nb * 8 + 8);
+    x.exits = c.take<int64_t>((size_t)x.nchunks * 8 + 8);
+    x.cnt = c.take<uint64_t>((size_t)(x.nchunks + 1) * 8);
+    x.base = c.take<uint64_t>((size_t)(x.nchunks + 1) * 8);
+    x.idx_err = c.take<int64_t>(8);
+    x.scan_tmp_bytes = need_index ? decode_scan_tmp_bytes(x.nchunks) : 0;
+    x.scan_tmp = c.take<void>(x.scan_tmp_bytes + 8);
+    if (b) *b = x;
+    return c.off;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    hipError_t alloc(size_t n, hipStream_t st) {
+        s = st;
+        return hipMallocAsync(&p, n ? n : 1, st);
+    }
+    ~DevBuf() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int bshuf_using_SSE2(void) { return 0; }
+int bshuf_using_NEON(void) { return 0; }
+int bshuf_using_AVX2(void) { return 0; }
+int bshuf_using_AVX512(void) { return 0; }
+int bshuf_using_HIP(void) { return have_device() ? 1 : 0; }
+
+// src/bitshuffle_core.c:2038-2046 -- format-stable, never change.
+size_t bshuf_default_block_size(const size_t elem_size) {
+    size_t bs = 8192 / elem_size;
+    bs = (bs / kBlockedMult) * kBlockedMult;
+    return bs > 128 ? bs : 128;
+}
+
+// src/bitshuffle.c:214-233, including its (size_t)-81 quirk.
+size_t bshuf_compress_lz4_bound(const size_t size, const size_t elem_size, size_t block_size) {
+    if (block_size == 0) block_size = bshuf_default_block_size(elem_size);
+    if (block_size % kBlockedMult) return (size_t)-81;
+    size_t bound = ((size_t)lz4_bound((int)(block_size * elem_size)) + 4) * (size / block_size);
+    size_t leftover = ((size % block_size) / kBlockedMult) * kBlockedMult;
+    if (leftover) bound += (size_t)lz4_bound((int)(leftover * elem_size)) + 4;
+    bound += (size % kBlockedMult) * elem_size;
+    return bound;
+}
+
+size_t bshuf_lz4_dev_nblocks(size_t size, size_t elem_size, size_t block_size) {
+    Plan p;
+    return make_plan(size, elem_size, block_size, p) == 0 ? (size_t)p.nb : 0;
+}
+
+// ---------------------------------------------------------------------------
+// device-resident entry points
+// ---------------------------------------------------------------------------
+
+static int64_t transpose_dev(const void* in, void* out, size_t size, size_t elem_size,
+                             size_t block_size, void* stream, bool fwd) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t* i8 = (const uint8_t*)in;
+    uint8_t* o8 = (uint8_t*)out;
+    if (launch_transpose(i8, o8, p.L, fwd, s) != hipSuccess) return kErrHip;
+    if (p.tail) {
+        const int64_t off = (p.L.nfull * (int64_t)p.L.bs + p.L.last) * p.L.E;
+        if (hipMemcpyAsync(o8 + off, i8 + off, (size_t)p.tail, hipMemcpyDeviceToDevice, s) !=
+            hipSuccess)
+            return kErrHip;
+    }
+    return (int64_t)(size * elem_size);
+}
+
+int64_t bshuf_bitshuffle_dev(const void* in, void* out, size_t size, size_t elem_size,
+                             size_t block_size, void* stream) {
+    return transpose_dev(in, out, size, elem_size, block_size, stream, true);
+}
+
+int64_t bshuf_bitunshuffle_dev(const void* in, void* out, size_t size, size_t elem_size,
+                               size_t block_size, void* stream) {
+    return transpose_dev(in, out, size, elem_size, block_size, stream, false);
+}
+
+size_t bshuf_compress_lz4_dev_workspace(size_t size, size_t elem_size, size_t block_size) {
+    Plan p;
+    if (make_plan(size, elem_size, block_size, p)) return 0;
+    return enc_ws(p, nullptr, nullptr);
+}
+
+int64_t bshuf_compress_lz4_dev(const void* in, void* out, size_t size, size_t elem_size,
+                               size_t block_size, void* ws, size_t ws_bytes, int64_t* d_result,
+                               uint64_t* block_offsets, void* stream) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
+    if (!have_device()) return kErrHip;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t need = enc_ws(p, nullptr, nullptr);
+    DevBuf own;
+    if (!ws) {
+        if (own.alloc(need, s) != hipSuccess) return -1;
+        ws = own.p;
+    } else if (ws_bytes < need || ((uintptr_t)ws & 255)) {
+        return kErrUnsupported;
+    }
+    EncodeBufs b;
+    enc_ws(p, &b, (uint8_t*)ws);
+    if (launch_encode((const uint8_t*)in, (uint8_t*)out, p.L, p.tail, b, d_result, s) !=
+        hipSuccess)
+        return kErrHip;
+    if (block_offsets && p.nb &&
+        hipMemcpyAsync(block_offsets, b.offs, (size_t)p.nb * 8, hipMemcpyDeviceToDevice, s) !=
+            hipSuccess)
+        return kErrHip;
+    return 0;
+}
+
+size_t bshuf_decompress_lz4_dev_workspace(size_t in_nbytes, size_t size, size_t elem_size,
+                                          size_t block_size) {
+    Plan p;
+    if (make_plan(size, elem_size, block_size, p)) return 0;
+    const int64_t cb = (int64_t)in_nbytes - p.tail;
+    return dec_ws(p, cb > 0 ? cb : 0, true, nullptr, nullptr);
+}
+
+int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, size_t size,
+                                 size_t elem_size, size_t block_size, void* ws, size_t ws_bytes,
+                                 int64_t* d_result, const uint64_t* block_offsets,
+                                 void* stream) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
+    if (!have_device()) return kErrHip;
+    hipStream_t s = (hipStream_t)stream;
+    int64_t cb = (int64_t)in_nbytes - p.tail;
+    if (cb < 0) cb = 0;
+    const bool need_index = block_offsets == nullptr;
+    const size_t need = dec_ws(p, cb, need_index, nullptr, nullptr);
+    DevBuf own;
+    if (!ws) {
+        if (own.alloc(need, s) != hipSuccess) return -1;
+        ws = own.p;
+    } else if (ws_bytes < need || ((uintptr_t)ws & 255)) {
+        return kErrUnsupported;
+    }
+    DecodeBufs b;
+    dec_ws(p, cb, need_index, &b, (uint8_t*)ws);
+    const uint8_t* i8 = (const uint8_t*)in;
+    if (need_index) {
+        if (launch_index(i8, cb, p.L, b, s) != hipSuccess) return kErrHip;
+    } else {
+        b.offs = const_cast<uint64_t*>(block_offsets);
+        b.idx_err = nullptr;
+    }
+    if (launch_decode(i8, (int64_t)in_nbytes, (uint8_t*)out, p.L, p.tail, b, d_result, s) !=
+        hipSuccess)
+        return kErrHip;
+    return 0;
+}
+
+int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first, uint64_t seed,
+                             void* stream) {
+    if (gen < 0 || gen > 2) return kErrUnsupported;
+    if (!have_device()) return kErrHip;
+    return launch_synth(out, n_elem, gen, first, seed, (hipStream_t)stream) == hipSuccess
+               ? 0
+               : kErrHip;
+}
+
+// ---------------------------------------------------------------------------
+// host-pointer drop-in entry points
+// ---------------------------------------------------------------------------
+
+static int64_t transpose_host(const void* in, void* out, size_t size, size_t elem_size,
+                              size_t block_size, bool fwd) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    const size_t bytes = size * elem_size;
+    if (bytes == 0) return 0;
+    hipStream_t s = thread_stream();
+    DevBuf di, dout;
+    if (di.alloc(bytes, s) != hipSuccess || dout.alloc(bytes, s) != hipSuccess) return -1;
+    if (hipMemcpyAsync(di.p, in, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return kErrHip;
+    const int64_t n = transpose_dev(di.p, dout.p, size, elem_size, block_size, s, fwd);
+    if (n < 0) return n;
+    if (hipMemcpyAsync(out, dout.p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return kErrHip;
+    if (hipStreamSynchronize(s) != hipSuccess) return kErrHip;
+    return n;
+}
+
+int64_t bshuf_bitshuffle(const void* in, void* out, const size_t size, const size_t elem_size,
+                         size_t block_size) {
+    return transpose_host(in, out, size, elem_size, block_size, true);
+}
+
+int64_t bshuf_bitunshuffle(const void* in, void* out, const size_t size, const size_t elem_size,
+                           size_t block_size) {
+    return transpose_host(in, out, size, elem_size, block_size, false);
+}
+
+int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const size_t elem_size,
+                           size_t block_size) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    const size_t bytes = size * elem_size;
+    const size_t bound = bshuf_compress_lz4_bound(size, elem_size, block_size);
+    hipStream_t s = thread_stream();
+    DevBuf di, dout, dres;
+    if (di.alloc(bytes, s) != hipSuccess || dout.alloc(bound, s) != hipSuccess ||
+        dres.alloc(8, s) != hipSuccess)
+        return -1;
+    if (bytes && hipMemcpyAsync(di.p, in, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+        return kErrHip;
+    const int64_t e = bshuf_compress_lz4_dev(di.p, dout.p, size, elem_size, block_size, nullptr, 0,
+                                             (int64_t*)dres.p, nullptr, s);
+    if (e < 0) return e;
+    int64_t res = 0;
+    if (hipMemcpyAsync(&res, dres.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return kErrHip;
+    if (res > 0 && (size_t)res <= bound) {
+        if (hipMemcpyAsync(out, dout.p, (size_t)res, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return kErrHip;
+    }
+    return res;
+}
+
+int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const size_t elem_size,
+                             size_t block_size) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
+    if (!have_device()) return kErrHip;
+    // Walk the BE32 headers through the host buffer (the reference's own
+    // iochain walk, src/bitshuffle.c:92-95) -- this also tells how many bytes
+    // of `in` belong to the stream, which the caller does not pass.
+    const uint8_t* i8 = (const uint8_t*)in;
+    std::vector<uint64_t> offs((size_t)p.nb);
+    uint64_t pos = 0;
+    for (int64_t k = 0; k < p.nb; k++) {
+        offs[(size_t)k] = pos;
+        const uint8_t* h = i8 + pos;
+        const uint32_t len = ((uint32_t)h[0] << 24) | ((uint32_t)h[1] << 16) |
+                             ((uint32_t)h[2] << 8) | h[3];
+        const int m = k < p.L.nfull ? p.L.bs : p.L.last;
+        if (len == 0 || len > (uint32_t)lz4_bound(m * p.L.E)) return -1000 - 1;
+        pos += 4 + (uint64_t)len;
+    }
+    const size_t in_nbytes = (size_t)pos + (size_t)p.tail;
+    const size_t bytes = size * elem_size;
+    hipStream_t s = thread_stream();
+    DevBuf di, dout, dres, doffs;
+    if (di.alloc(in_nbytes, s) != hipSuccess || dout.alloc(bytes, s) != hipSuccess ||
+        dres.alloc(8, s) != hipSuccess || doffs.alloc((size_t)p.nb * 8, s) != hipSuccess)
+        return -1;
+    if ((in_nbytes && hipMemcpyAsync(di.p, in, in_nbytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (p.nb && hipMemcpyAsync(doffs.p, offs.data(), (size_t)p.nb * 8, hipMemcpyHostToDevice, s) !=
+                     hipSuccess))
+        return kErrHip;
+    const int64_t e = bshuf_decompress_lz4_dev(di.p, in_nbytes, dout.p, size, elem_size, block_size,
+                                               nullptr, 0, (int64_t*)dres.p,
+                                               (const uint64_t*)doffs.p, s);
+    if (e < 0) return e;
+    int64_t res = 0;
+    if (hipMemcpyAsync(&res, dres.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return kErrHip;
+    if (res >= 0 && bytes) {
+        if (hipMemcpyAsync(out, dout.p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return kErrHip;
+    }
+    return res;
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+// launch.h -- host-side launchers for the gfx950 kernels (internal to the .so).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "bshuf_dev.h"
+
+namespace bshuf {
+
+// Transpose tiles: 256 groups (2048 elements) per 256-thread workgroup.
+constexpr int kTileGroups = 256;
+
+// bitshuffle / bitunshuffle of all full + partial blocks (tail not included).
+hipError_t launch_transpose(const uint8_t* in, uint8_t* out, const Layout& L, bool forward,
+                            hipStream_t s);
+
+// ---- LZ4 encode --------------------------------------------------------
+struct EncodeBufs {
+    uint8_t* scratch;   // nblocks * slot bytes: [BE32 c][c payload] per block
+    int64_t slot;       // bytes per scratch slot (16-aligned, >= 4 + lz4_bound)
+    uint64_t* foot;     // nblocks + 1 u64: 4 + c per block, last = 0
+    uint64_t* offs;     // nblocks + 1 u64: exclusive scan of foot
+    void* scan_tmp;     // hipcub temp storage
+    size_t scan_tmp_bytes;
+};
+size_t encode_scan_tmp_bytes(int64_t nblocks);
+int64_t encode_slot_bytes(const Layout& L);
+hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64_t tail_bytes,
+                         const EncodeBufs& b, int64_t* d_result, hipStream_t s);
+// Largest block (bytes) the LDS-resident encoder/decoder accepts.
+int64_t max_device_block_bytes();
+
+// ---- LZ4 decode --------------------------------------------------------
+struct DecodeBufs {
+    uint64_t* offs;     // nblocks u64: header offset of each block
+    int64_t* status;    // nblocks i64: consumed bytes or error code per block
+    // block index rebuild (unused when offsets are supplied)
+    int64_t* exits;     // nchunks
+    uint64_t* cnt;      // nchunks + 1
+    uint64_t* base;     // nchunks + 1
+    int64_t* idx_err;   // 1 word
+    void* scan_tmp;
+    size_t scan_tmp_bytes;
+    int64_t chunk;      // chunk bytes for the index rebuild
+    int64_t nchunks;
+};
+int64_t index_chunk_bytes(const Layout& L);
+size_t decode_scan_tmp_bytes(int64_t nchunks);
+hipError_t launch_index(const uint8_t* in, int64_t blocks_end, const Layout& L,
+                        const DecodeBufs& b, hipStream_t s);
+hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
+                         int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
+                         hipStream_t s);
+
+// ---- synthetic inputs ----------------------------------------------------
+hipError_t launch_synth(void* out, size_t n, int gen, uint64_t first, uint64_t seed,
+                        hipStream_t s);
+
+}  // namespace bshuf

@@ -1,0 +1,76 @@
+/*
+ * bitshuffle.h -- drop-in C-ABI for bitshuffle + LZ4 (framed stream), served
+ * by hand-written HIP kernels on MI355X (gfx950).
+ *
+ * Replaces (same names, signatures, argument meaning, return values):
+ *   bshuf_compress_lz4_bound   src/bitshuffle.h:58-74  (impl src/bitshuffle.c:214-233)
+ *   bshuf_compress_lz4         src/bitshuffle.h:77-98  (impl src/bitshuffle.c:236-240)
+ *   bshuf_decompress_lz4       src/bitshuffle.h:101-116 (impl src/bitshuffle.c:243-247)
+ * Stream format (bit-exact with the reference): for each block of block_size
+ * elements (then one partial block of (size % block_size) & ~7 elements)
+ *   u32 big-endian  c   ||  c bytes of LZ4 v1.10.0 block (LZ4_compress_default)
+ * of the block's bit-transposed bytes, followed by (size % 8) * elem_size raw
+ * bytes.  bshuf_compress_lz4 returns bytes written; bshuf_decompress_lz4
+ * returns bytes CONSUMED from `in`.  ZSTD entry points are out of scope.
+ */
+#ifndef BITSHUFFLE_H
+#define BITSHUFFLE_H
+
+#include "bitshuffle_core.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+size_t bshuf_compress_lz4_bound(const size_t size, const size_t elem_size, size_t block_size);
+
+int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size,
+                           const size_t elem_size, size_t block_size);
+
+int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size,
+                             const size_t elem_size, size_t block_size);
+
+/* ---- device-resident extensions (additive, not in the reference) ----
+ *
+ * Workspace: pass ws=NULL to let the library allocate (stream-ordered) per
+ * call, or pre-allocate bshuf_*_dev_workspace() bytes of device memory (must
+ * be 256-byte aligned) so the call performs no allocation and can be captured
+ * into a hipGraph.
+ *
+ * Results are written to *d_result (a DEVICE int64): bytes written (compress),
+ * bytes consumed (decompress), or a negative error code.  The call itself
+ * returns 0 once the work is enqueued, or a negative code for host-detected
+ * argument errors.  Nothing synchronises.
+ *
+ * bshuf_decompress_lz4_dev needs `in_nbytes`, the number of readable bytes at
+ * `in` (the reference's host API walks headers through the buffer instead;
+ * on the device the block index is rebuilt in parallel from the framing and
+ * in_nbytes bounds every read).  `block_offsets` (optional, may be NULL) lets
+ * a caller that kept the encoder's index skip that rebuild: bshuf_compress_lz4_dev
+ * fills it when non-NULL (nblocks u64 entries = byte offset of each block header).
+ */
+size_t bshuf_compress_lz4_dev_workspace(size_t size, size_t elem_size, size_t block_size);
+size_t bshuf_decompress_lz4_dev_workspace(size_t in_nbytes, size_t size, size_t elem_size,
+                                          size_t block_size);
+size_t bshuf_lz4_dev_nblocks(size_t size, size_t elem_size, size_t block_size);
+
+int64_t bshuf_compress_lz4_dev(const void* in, void* out, size_t size, size_t elem_size,
+                               size_t block_size, void* ws, size_t ws_bytes,
+                               int64_t* d_result, uint64_t* block_offsets, void* stream);
+
+int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, size_t size,
+                                 size_t elem_size, size_t block_size, void* ws,
+                                 size_t ws_bytes, int64_t* d_result,
+                                 const uint64_t* block_offsets, void* stream);
+
+/* Synthetic benchmark inputs of SURVEY.md 8(d), generated on the device
+ * (counter based, identical to the CPU definition): gen 0 = int32 ramp,
+ * 1 = int16 correlated noise (G1), 2 = float32 smooth field (G2). */
+int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first,
+                             uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BITSHUFFLE_H */

@@ -1,0 +1,234 @@
+"""Parity of the HIP path (through the C-ABI) with the reference.
+
+Checked against: the reference's 42 LZ4 regression chunks, the
+reference-generated vectors of tests/golden/vectors.json, the CPU oracle on
+seeded random/odd/edge inputs, and at BASELINE sizes against SHA-256 digests
+of the reference's own output.  Integer/byte work: every comparison is
+bit-exact.
+"""
+import numpy as np
+import pytest
+
+from tests.vectors import compressed, load_vectors, make_input, regression_cases, sha
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}
+
+
+def view_e(data, E):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    return data.view(DTYPES[E]) if E in DTYPES else data.view(np.dtype("V%d" % E))
+
+
+@pytest.fixture(scope="module")
+def bs():
+    import bitshuffle_amd
+    assert bitshuffle_amd.using_HIP(), "no HIP device: the GPU suite must run on MI355X"
+    return bitshuffle_amd
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+# ------------------------------------------------------------------ transpose
+@pytest.mark.parametrize("E", [1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 24])
+def test_bitshuffle_matches_oracle(bs, oracle, E):
+    rng = np.random.default_rng(100 + E)
+    for n in [0, 1, 7, 8, 9, 64, 100, 1000, 4097, 33000]:
+        for block in [0, 8, 64, 680, 2048]:
+            arr = view_e(rng.integers(0, 256, n * E, dtype=np.uint8), E)
+            want = oracle.bitshuffle(arr, block)
+            got = bs.bitshuffle(arr, block)
+            assert got.tobytes() == want.tobytes(), (E, n, block)
+            back = bs.bitunshuffle(got, block)
+            assert back.tobytes() == arr.tobytes(), (E, n, block)
+
+
+def test_bitshuffle_golden_and_known_answer(bs, oracle):
+    from tests.test_oracle import trans_bit_elem_np
+    for spec in load_vectors()["small"]:
+        a = make_input(oracle, spec)
+        assert sha(bs.bitshuffle(a, spec["bs"])) == spec["shuffled_sha256"], spec["name"]
+    rng = np.random.default_rng(7)
+    for dt in [np.int8, np.int16, np.int32, np.int64, np.dtype("V3"), np.dtype("V12")]:
+        dt = np.dtype(dt)
+        arr = rng.integers(0, 200, 1024 * dt.itemsize, dtype=np.uint8).view(dt)
+        # a single block covering the whole array == trans_bit_elem of test_ext.py:702-716
+        got = bs.bitshuffle(arr, arr.size)
+        assert got.tobytes() == trans_bit_elem_np(arr).tobytes(), dt
+
+
+def test_bitshuffle_bad_block_size(bs):
+    with pytest.raises(RuntimeError) as ei:
+        bs.bitshuffle(np.arange(100, dtype=np.int16), 12)
+    assert ei.value.args[1] == -81
+
+
+# ------------------------------------------------------------------ LZ4 stream
+def test_regression_chunks_encode_decode(bs):
+    """The 42 stored LZ4 chunks of the reference's regression files
+    (tests/test_regression.py:24-42): decode to `original`, and re-encoding
+    `original` reproduces the stored bytes exactly."""
+    cases = regression_cases()
+    assert len(cases) == 42
+    for ver, name, arr, chunk, block in cases:
+        stream = chunk[12:]
+        dec = bs.decompress_lz4(stream, arr.shape, arr.dtype, block)
+        assert dec.tobytes() == arr.tobytes(), (ver, name)
+        enc = bs.compress_lz4(arr, block)
+        assert enc.tobytes() == stream.tobytes(), (ver, name)
+
+
+def test_golden_vectors_encode_decode(bs, oracle):
+    for spec in load_vectors()["small"]:
+        a = make_input(oracle, spec)
+        ref = compressed(spec)
+        enc = bs.compress_lz4(a, spec["bs"])
+        assert enc.size == spec["compressed_len"], spec["name"]
+        assert enc.tobytes() == ref.tobytes(), spec["name"]
+        dec = bs.decompress_lz4(ref, a.shape, a.dtype, spec["bs"])
+        assert dec.tobytes() == a.tobytes(), spec["name"]
+
+
+@pytest.mark.parametrize("kind", ["random", "runs", "periodic", "walk", "zeros"])
+def test_lz4_matches_oracle(bs, oracle, kind):
+    rng = np.random.default_rng(hash(kind) & 0xFFFF)
+    for E in [1, 2, 4, 8, 3, 12]:
+        for n in [1, 8, 13, 64, 200, 1000, 5000, 40000]:
+            nbytes = n * E
+            if kind == "random":
+                d = rng.integers(0, 256, nbytes, dtype=np.uint8)
+            elif kind == "runs":
+                d = np.repeat(rng.integers(0, 4, nbytes // 7 + 1), 7)[:nbytes].astype(np.uint8)
+            elif kind == "periodic":
+                d = (np.arange(nbytes) % (1 + (n % 13)) * 29).astype(np.uint8)
+            elif kind == "walk":
+                d = (rng.integers(-2, 3, nbytes).cumsum() % 256).astype(np.uint8)
+            else:
+                d = np.zeros(nbytes, dtype=np.uint8)
+            arr = view_e(d, E)
+            for block in [0, 64, 8]:
+                want = oracle.compress_lz4(arr, block)
+                got = bs.compress_lz4(arr, block)
+                assert got.tobytes() == want.tobytes(), (kind, E, n, block)
+                back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
+                assert back.tobytes() == arr.tobytes(), (kind, E, n, block)
+
+
+def test_lz4_u32_table_path(bs, oracle):
+    """Blocks of >= 65547 bytes switch LZ4 to the byU32 table + hash5
+    (lz4/lz4.c:1389-1393, 785-795)."""
+    g1 = oracle.gen_g1(1 << 19)
+    for arr, block in [(g1.view(np.uint64), 8200), (g1, 40000), (g1, 32768 + 8),
+                       (oracle.gen_g2(1 << 17), 16400)]:
+        want = oracle.compress_lz4(arr, block)
+        got = bs.compress_lz4(arr, block)
+        assert got.tobytes() == want.tobytes(), (arr.dtype, block)
+        back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
+        assert back.tobytes() == arr.tobytes()
+
+
+def test_decompress_errors(bs, oracle):
+    arr = oracle.gen_g1(10000)
+    enc = oracle.compress_lz4(arr)
+    bad = enc.copy()
+    bad[4 + 20] ^= 0xFF  # corrupt the first block's payload
+    with pytest.raises(RuntimeError):
+        out = bs.decompress_lz4(bad, arr.shape, arr.dtype)
+        assert out.tobytes() != arr.tobytes()
+        raise RuntimeError("corrupt stream decoded to different data")
+    with pytest.raises(RuntimeError):
+        bs.decompress_lz4(enc[:-1], arr.shape, arr.dtype)  # consumed != buffer size
+
+
+# ------------------------------------------------------------------ device API
+def test_device_api_roundtrip_and_index(bs, oracle, torch):
+    for spec in load_vectors()["small"]:
+        a = make_input(oracle, spec)
+        ref = compressed(spec)
+        t = torch.from_numpy(a.view(np.uint8).copy()).cuda()
+        off = torch.empty(max(1, bs.lib.bshuf_lz4_dev_nblocks(a.size, a.dtype.itemsize, spec["bs"])),
+                          dtype=torch.int64, device="cuda")
+        # element count / size come from the original dtype
+        out = torch.empty(bs.compress_lz4_bound(a.size, a.dtype.itemsize, spec["bs"]),
+                          dtype=torch.uint8, device="cuda")
+        res = torch.empty(1, dtype=torch.int64, device="cuda")
+        import ctypes
+        rc = bs.lib.bshuf_compress_lz4_dev(ctypes.c_void_p(t.data_ptr()),
+                                           ctypes.c_void_p(out.data_ptr()), a.size,
+                                           a.dtype.itemsize, spec["bs"], None, 0,
+                                           ctypes.c_void_p(res.data_ptr()),
+                                           ctypes.c_void_p(off.data_ptr()), None)
+        assert rc == 0
+        n = int(res.item())
+        assert n == ref.size, spec["name"]
+        assert out[:n].cpu().numpy().tobytes() == ref.tobytes(), spec["name"]
+        # decode with the parallel index rebuild (no offsets)
+        dec = torch.empty(a.size * a.dtype.itemsize, dtype=torch.uint8, device="cuda")
+        rc = bs.lib.bshuf_decompress_lz4_dev(ctypes.c_void_p(out.data_ptr()), n,
+                                             ctypes.c_void_p(dec.data_ptr()), a.size,
+                                             a.dtype.itemsize, spec["bs"], None, 0,
+                                             ctypes.c_void_p(res.data_ptr()), None, None)
+        assert rc == 0
+        assert int(res.item()) == n, spec["name"]
+        assert dec.cpu().numpy().tobytes() == a.view(np.uint8).tobytes(), spec["name"]
+        # decode with the encoder's offsets
+        dec.zero_()
+        rc = bs.lib.bshuf_decompress_lz4_dev(ctypes.c_void_p(out.data_ptr()), n,
+                                             ctypes.c_void_p(dec.data_ptr()), a.size,
+                                             a.dtype.itemsize, spec["bs"], None, 0,
+                                             ctypes.c_void_p(res.data_ptr()),
+                                             ctypes.c_void_p(off.data_ptr()), None)
+        assert rc == 0 and int(res.item()) == n
+        assert dec.cpu().numpy().tobytes() == a.view(np.uint8).tobytes(), spec["name"]
+
+
+def test_device_synth_matches_cpu_generators(bs, oracle, torch):
+    for gen, dt, ref in [(0, torch.int32, oracle.gen_g0), (1, torch.int16, oracle.gen_g1),
+                         (2, torch.float32, oracle.gen_g2)]:
+        t = torch.empty(100003, dtype=dt, device="cuda")
+        bs.synth_fill_dev(t, gen, first=12345678)
+        want = ref(100003, 12345678) if gen == 0 else ref(100003, 12345678, 12345)
+        assert t.cpu().numpy().tobytes() == want.tobytes(), gen
+
+
+# ------------------------------------------------------------------ full size
+@pytest.mark.slow
+def test_full_size_digests(bs, torch):
+    """BASELINE configs 1, 2 and 4 at full size vs SHA-256 of the reference's
+    output (tests/golden/vectors.json 'full'), plus decode round trips."""
+    import hashlib
+    full = {e["name"]: e for e in load_vectors()["full"]}
+
+    def digest(t):
+        h = hashlib.sha256()
+        step = 1 << 28
+        for i in range(0, t.numel(), step):
+            h.update(t[i:i + step].cpu().numpy().tobytes())
+        return h.hexdigest()
+
+    e = full["cfg1_g0_i32_64MiB"]
+    x = torch.empty(e["size"], dtype=torch.int32, device="cuda")
+    bs.synth_fill_dev(x, 0)
+    assert digest(x.view(torch.uint8)) == e["input_sha256"]
+    y = bs.bitshuffle_dev(x)
+    assert digest(y.view(torch.uint8)) == e["shuffled_sha256"]
+    assert torch.equal(bs.bitunshuffle_dev(y), x)
+    del x, y
+
+    for name in ["cfg4_g1_chunk0000", "cfg4_g1_chunk1023", "cfg2_g1_i16_4GiB"]:
+        e = full[name]
+        x = torch.empty(e["size"], dtype=torch.int16, device="cuda")
+        bs.synth_fill_dev(x, 1, seed=e.get("seed", 12345))
+        c = bs.compress_lz4_dev(x)
+        assert c.numel() == e["compressed_len"], name
+        assert digest(c) == e["compressed_sha256"], name
+        d = bs.decompress_lz4_dev(c.clone(), x.shape, x.dtype)
+        assert torch.equal(d, x), name
+        del x, c, d
+        torch.cuda.empty_cache()
