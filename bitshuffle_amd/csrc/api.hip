@@ -98,6 +98,7 @@ size_t dec_ws(const Plan& p, int64_t blocks_end, bool need_index, DecodeBufs* b,
     x.cnt = c.take<uint64_t>((size_t)(x.nchunks + 1) * 8);
     x.base = c.take<uint64_t>((size_t)(x.nchunks + 1) * 8);
     x.idx_err = c.take<int64_t>(8);
+    x.bad = c.take<long long>(8);
     x.scan_tmp_bytes = need_index ? decode_scan_tmp_bytes(x.nchunks) : 0;
     x.scan_tmp = c.take<void>(x.scan_tmp_bytes + 8);
     if (b) *b = x;

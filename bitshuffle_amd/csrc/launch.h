@@ -9,6 +9,23 @@
 
 namespace bshuf {
 
+// Per-kernel event timing (prof.hip); a no-op unless bshuf_prof_enable(1).
+bool prof_on();
+class ProfScope {
+  public:
+    ProfScope(const char* name, hipStream_t s);
+    ~ProfScope();
+
+  private:
+    const char* name_;
+    hipStream_t s_;
+    void* a_;
+};
+
+// Workgroups for a persistent launch: resident blocks per CU (occupancy API,
+// dynamic LDS included) x CUs of the current device, capped by the work.
+int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work);
+
 // Transpose tiles: 256 groups (2048 elements) per 256-thread workgroup.
 constexpr int kTileGroups = 256;
 
@@ -41,6 +58,7 @@ struct DecodeBufs {
     uint64_t* cnt;      // nchunks + 1
     uint64_t* base;     // nchunks + 1
     int64_t* idx_err;   // 1 word
+    long long* bad;     // 1 word: highest failing block index
     void* scan_tmp;
     size_t scan_tmp_bytes;
     int64_t chunk;      // chunk bytes for the index rebuild

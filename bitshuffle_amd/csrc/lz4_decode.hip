@@ -249,89 +249,171 @@ struct DecArgs {
     const uint64_t* offs;
     uint8_t* out;
     int64_t* status;
+    long long* bad;  // highest failing block index (init -1)
     Layout L;
     uint32_t maxlen;
-    int32_t cap;  // bytes reserved for the compressed block in LDS
+    int32_t cap;     // LDS bytes reserved for the decoded block
 };
 
+// Byte range [o0, o1) of block k's record ([BE32 c][c bytes]) in the stream.
+// Consecutive records are contiguous, so the next offset ends this record;
+// the last record is bounded by its worst-case size.
+struct Span {
+    int64_t o0, o1;
+};
+
+__device__ __forceinline__ Span span_of(const DecArgs& a, int64_t k, int64_t nb) {
+    Span sp;
+    sp.o0 = (int64_t)a.offs[k];
+    sp.o1 = (k + 1 < nb) ? (int64_t)a.offs[k + 1] : sp.o0 + 4 + (int64_t)a.maxlen;
+    if (sp.o1 > a.in_nbytes) sp.o1 = a.in_nbytes;
+    if (sp.o0 > sp.o1) sp.o0 = sp.o1;
+    return sp;
+}
+
+// 16-byte chunks covering a record of an 8 KiB block: (8244 + 30) / 16 / 64 -> 9.
+constexpr int kPayIters = 9;
+
+struct PayRegs {
+    uint4 v[kPayIters];
+};
+
+__device__ __forceinline__ bool span_fits(const Span& sp) {
+    const int64_t a0 = sp.o0 & ~(int64_t)15;
+    return ((sp.o1 - a0 + 15) >> 4) <= kPayIters * kWave;
+}
+
+// Loads the 16-byte-aligned chunks covering [o0, o1); chunks that reach past
+// in_nbytes are assembled bytewise so nothing is read outside the stream.
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* in, int64_t in_nbytes, int64_t gb) {
+    if (gb + 16 <= in_nbytes) return *reinterpret_cast<const uint4*>(in + gb);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int j = 0; j < 16; j++)
+        if (gb + j < in_nbytes) w[j >> 2] |= (uint32_t)in[gb + j] << (8 * (j & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Span& sp, int lane) {
+    const int64_t a0 = sp.o0 & ~(int64_t)15;
+    const int nch = (int)((sp.o1 - a0 + 15) >> 4);
+#pragma unroll
+    for (int it = 0; it < kPayIters; it++) {
+        const int c = it * kWave + lane;
+        if (c < nch) R.v[it] = load_chunk(a.in, a.in_nbytes, a0 + 16 * (int64_t)c);
+    }
+}
+
+__device__ __forceinline__ void land_pay(const PayRegs& R, const Span& sp, uint8_t* C, int lane) {
+    const int64_t a0 = sp.o0 & ~(int64_t)15;
+    const int nch = (int)((sp.o1 - a0 + 15) >> 4);
+#pragma unroll
+    for (int it = 0; it < kPayIters; it++) {
+        const int c = it * kWave + lane;
+        if (c < nch) reinterpret_cast<uint4*>(C)[c] = R.v[it];
+    }
+}
+
+// Persistent: workgroup w decodes blocks w, w+G, ...  Offsets are fetched two
+// blocks ahead and the next record's bytes one block ahead, into registers,
+// so HBM latency overlaps the LDS-bound LZ4 parse of the current block.
 template <int EK>
-__global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a) {
+__global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
-    const int64_t blk = blockIdx.x;
     const int E = EK ? EK : a.L.E;
-    const int m = blk < a.L.nfull ? a.L.bs : a.L.last;
-    const int n = m * E;
-    const int P = m / 8;
-    uint8_t* D = smem;                 // decoded (shuffled) block
-    uint8_t* Cl = smem + a.cap + 16;   // compressed block (16-aligned), +shift
-    const int64_t h = (int64_t)a.offs[blk];
-    int status = 0;
-    int clen = 0;
-    if (h + 4 > a.in_nbytes) {
-        status = -1000 - 1;
-    } else {
-        clen = (int)be32_global(a.in + h);
-        if (clen <= 0 || (uint32_t)clen > a.maxlen || h + 4 + clen > a.in_nbytes) status = -1000 - 1;
-    }
-    if (status == 0) {
-        // stage the compressed block in LDS with aligned dword loads
-        const int64_t start = h + 4;
-        const int64_t a0 = start & ~(int64_t)3;
-        const int shift = (int)(start - a0);
-        const int64_t end = start + clen;
-        const int nw = (int)((end - a0 + 3) >> 2);
-        const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.in + a0);
-        uint32_t* l32 = reinterpret_cast<uint32_t*>(Cl);
-        for (int i = lane; i < nw; i += kWave) {
-            const int64_t gb = a0 + 4 * (int64_t)i;
-            uint32_t v;
-            if (gb + 4 <= a.in_nbytes) {
-                v = g32[i];
-            } else {
-                v = 0;
-                for (int j = 0; j < 4; j++)
-                    if (gb + j < a.in_nbytes) v |= (uint32_t)a.in[gb + j] << (8 * j);
-            }
-            l32[i] = v;
+    uint8_t* D = smem;                     // decoded (bit-shuffled) block
+    uint8_t* Cbuf = smem + a.cap + 16;     // record bytes, 16-aligned base
+    const int64_t stride = gridDim.x;
+    int64_t blk = blockIdx.x;
+    if (blk >= nb) return;
+
+    Span cur = span_of(a, blk, nb);
+    Span nxt = {0, 0};
+    if (blk + stride < nb) nxt = span_of(a, blk + stride, nb);
+    PayRegs R;
+    bool cur_in_regs = span_fits(cur);
+    if (cur_in_regs) issue_pay(R, a, cur, lane);
+
+    for (;;) {
+        const int m = blk < a.L.nfull ? a.L.bs : a.L.last;
+        const int n = m * E;
+        const int P = m / 8;
+        // land this record in LDS
+        if (cur_in_regs) {
+            land_pay(R, cur, Cbuf, lane);
+        } else {
+            const int64_t a0 = cur.o0 & ~(int64_t)15;
+            const int nch = (int)((cur.o1 - a0 + 15) >> 4);
+            for (int c = lane; c < nch; c += kWave)
+                reinterpret_cast<uint4*>(Cbuf)[c] = load_chunk(a.in, a.in_nbytes, a0 + 16 * (int64_t)c);
         }
-        __syncthreads();
-        const int r = lz4_decode_block(reinterpret_cast<const uint8_t*>(l32) + shift, clen, D, n, lane);
-        if (r == -91)
-            status = -91;
-        else if (r < 0)
-            status = r - 1000;
-    }
-    if (status == 0) {
-        __syncthreads();
-        uint8_t* dst = a.out + blk * (int64_t)a.L.bs * E;
-        if constexpr (EK != 0) {
-            for (int g = lane; g < P; g += kWave) {
-                uint32_t w[2 * EK];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // prefetch: next record into registers, the one after into `nxt2`
+        const int64_t next = blk + stride;
+        const bool next_in_regs = next < nb && span_fits(nxt);
+        if (next_in_regs) issue_pay(R, a, nxt, lane);
+        Span nxt2 = {0, 0};
+        if (next + stride < nb) nxt2 = span_of(a, next + stride, nb);
+
+        const uint8_t* C = Cbuf + (cur.o0 & 15);
+        const int avail = (int)(cur.o1 - cur.o0);
+        int status = 0, clen = 0;
+        if (avail < 4) {
+            status = -1000 - 1;
+        } else {
+            clen = (int)be32_load(C);
+            const bool last = blk + 1 == nb;
+            if (clen <= 0 || (uint32_t)clen > a.maxlen || clen + 4 > avail ||
+                (!last && clen + 4 != avail))
+                status = (clen + 4 > avail) ? -1000 - 1 : -91;
+        }
+        if (status == 0) {
+            const int r = lz4_decode_block(C + 4, clen, D, n, lane);
+            status = (r == -91) ? -91 : (r < 0 ? r - 1000 : 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (status == 0) {
+            uint8_t* dst = a.out + blk * (int64_t)a.L.bs * E;
+            if constexpr (EK != 0) {
+                for (int g = lane; g < P; g += kWave) {
+                    uint32_t w[2 * EK];
 #pragma unroll
-                for (int i = 0; i < 2 * EK; i++) w[i] = 0;
+                    for (int i = 0; i < 2 * EK; i++) w[i] = 0;
 #pragma unroll
-                for (int b = 0; b < EK; b++) {
+                    for (int b = 0; b < EK; b++) {
+                        uint64_t v = 0;
+#pragma unroll
+                        for (int j = 0; j < 8; j++) v |= (uint64_t)D[(8 * b + j) * P + g] << (8 * j);
+                        scatter_byte_plane<EK>(w, b, tr8x8(v));
+                    }
+                    store_group<EK>(dst + (int64_t)g * 8 * EK, w);
+                }
+            } else {
+                for (int i = lane; i < P * E; i += kWave) {
+                    const int g = i / E, b = i - g * E;
                     uint64_t v = 0;
 #pragma unroll
                     for (int j = 0; j < 8; j++) v |= (uint64_t)D[(8 * b + j) * P + g] << (8 * j);
-                    scatter_byte_plane<EK>(w, b, tr8x8(v));
+                    v = tr8x8(v);
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        dst[(int64_t)(8 * g + k) * E + b] = (uint8_t)(v >> (8 * k));
                 }
-                store_group<EK>(dst + (int64_t)g * 8 * EK, w);
             }
-        } else {
-            for (int i = lane; i < P * E; i += kWave) {
-                const int g = i / E, b = i - g * E;
-                uint64_t v = 0;
-#pragma unroll
-                for (int j = 0; j < 8; j++) v |= (uint64_t)D[(8 * b + j) * P + g] << (8 * j);
-                v = tr8x8(v);
-#pragma unroll
-                for (int k = 0; k < 8; k++) dst[(int64_t)(8 * g + k) * E + b] = (uint8_t)(v >> (8 * k));
-            }
+        } else if (lane == 0) {
+            atomicMax(a.bad, (long long)blk);
         }
+        if (lane == 0) a.status[blk] = status == 0 ? (int64_t)clen + 4 : (int64_t)status;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (next >= nb) break;
+        blk = next;
+        cur = nxt;
+        nxt = nxt2;
+        cur_in_regs = next_in_regs;
     }
-    if (lane == 0) a.status[blk] = status == 0 ? (int64_t)clen + 4 : (int64_t)status;
 }
 
 // Result: bytes consumed, or the error of the LAST failing block (the
@@ -339,24 +421,20 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a) {
 // Also copies the raw tail (whose position is only known from the index).
 __global__ __launch_bounds__(256) void k_decode_finish(const int64_t* __restrict__ status,
                                                        const uint64_t* __restrict__ offs,
-                                                       int64_t nblocks, const int64_t* idx_err,
-                                                       const uint8_t* in, int64_t in_nbytes,
-                                                       uint8_t* tail_dst, int64_t tail,
-                                                       int64_t* result) {
-    __shared__ long long last_bad;
-    if (threadIdx.x == 0) last_bad = -1;
-    __syncthreads();
-    for (int64_t k = threadIdx.x; k < nblocks; k += blockDim.x)
-        if (status[k] < 0) atomicMax(&last_bad, (long long)k);
-    __syncthreads();
+                                                       int64_t nblocks, const long long* bad,
+                                                       const int64_t* idx_err, const uint8_t* in,
+                                                       int64_t in_nbytes, uint8_t* tail_dst,
+                                                       int64_t tail, int64_t* result) {
+    const long long last_bad = *bad;
     const int64_t end = nblocks ? (int64_t)offs[nblocks - 1] + status[nblocks - 1] : 0;
     const bool idx_bad = idx_err && *idx_err != 0;
-    if (last_bad < 0 && !idx_bad && end + tail <= in_nbytes)
+    const bool ok = last_bad < 0 && !idx_bad && end + tail <= in_nbytes;
+    if (ok)
         for (int64_t i = threadIdx.x; i < tail; i += blockDim.x) tail_dst[i] = in[end + i];
     if (threadIdx.x == 0) {
         if (last_bad >= 0)
             *result = status[last_bad];
-        else if (idx_bad || end + tail > in_nbytes)
+        else if (!ok)
             *result = -91;
         else
             *result = end + tail;
@@ -387,18 +465,30 @@ hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const De
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     const int64_t W = 4 + (int64_t)maxlen;
     const int64_t nch = b.nchunks;
-    hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), 0, s, in, Cb, b.chunk, W,
-                       maxlen, b.exits);
+    {
+        ProfScope prof("k_idx_exits", s);
+        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), 0, s, in, Cb, b.chunk, W,
+                           maxlen, b.exits);
+    }
     const unsigned wg = (unsigned)((nch + 63) / 64);
-    hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, in, Cb, b.chunk, maxlen, b.exits,
-                       b.cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr, nb, b.idx_err, 0);
+    {
+        ProfScope prof("k_idx_walk_count", s);
+        hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, in, Cb, b.chunk, maxlen, b.exits,
+                           b.cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr, nb, b.idx_err, 0);
+    }
     e = hipMemsetAsync(b.cnt + nch, 0, sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     size_t tmp = b.scan_tmp_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.cnt, b.base, (int)(nch + 1), s);
+    {
+        ProfScope prof("scan_chunk_counts", s);
+        e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.cnt, b.base, (int)(nch + 1), s);
+    }
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, in, Cb, b.chunk, maxlen, b.exits,
-                       b.cnt, b.base, b.offs, nb, b.idx_err, 1);
+    {
+        ProfScope prof("k_idx_walk_write", s);
+        hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, in, Cb, b.chunk, maxlen, b.exits,
+                           b.cnt, b.base, b.offs, nb, b.idx_err, 1);
+    }
     hipLaunchKernelGGL(k_idx_check, dim3(1), dim3(64), 0, s, b.base, nch, nb, b.idx_err);
     return hipGetLastError();
 }
@@ -407,11 +497,14 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
                          hipStream_t s) {
     const int64_t nb = L.nblocks();
+    hipError_t e = hipMemsetAsync(b.bad, 0xFF, sizeof(long long), s);  // -1
+    if (e != hipSuccess) return e;
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
-        DecArgs a{in, in_nbytes, b.offs, out, b.status, L, (uint32_t)lz4_bound((int)nmax),
+        DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
                   (int32_t)((nmax + 15) & ~15)};
-        const size_t lds = (size_t)a.cap + 16 + ((a.maxlen + 8 + 15) & ~15u) + 16;
+        // decoded block + record (header, payload, 16-byte alignment slack)
+        const size_t lds = (size_t)a.cap + 16 + (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
         const bool aligned = ((uintptr_t)out & 15) == 0;
         const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
         const void* fn = nullptr;
@@ -423,23 +516,26 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
             default: fn = reinterpret_cast<const void*>(k_lz4_decode<0>); break;
         }
         if (lds > 65536) {
-            hipError_t e =
-                hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
+        const dim3 grid((unsigned)persistent_grid(fn, kWave, lds, nb));
+        ProfScope prof("k_lz4_decode", s);
         switch (ek) {
-            case 1: hipLaunchKernelGGL(k_lz4_decode<1>, dim3((unsigned)nb), dim3(kWave), lds, s, a); break;
-            case 2: hipLaunchKernelGGL(k_lz4_decode<2>, dim3((unsigned)nb), dim3(kWave), lds, s, a); break;
-            case 4: hipLaunchKernelGGL(k_lz4_decode<4>, dim3((unsigned)nb), dim3(kWave), lds, s, a); break;
-            case 8: hipLaunchKernelGGL(k_lz4_decode<8>, dim3((unsigned)nb), dim3(kWave), lds, s, a); break;
-            default: hipLaunchKernelGGL(k_lz4_decode<0>, dim3((unsigned)nb), dim3(kWave), lds, s, a); break;
+            case 1: hipLaunchKernelGGL(k_lz4_decode<1>, grid, dim3(kWave), lds, s, a, nb); break;
+            case 2: hipLaunchKernelGGL(k_lz4_decode<2>, grid, dim3(kWave), lds, s, a, nb); break;
+            case 4: hipLaunchKernelGGL(k_lz4_decode<4>, grid, dim3(kWave), lds, s, a, nb); break;
+            case 8: hipLaunchKernelGGL(k_lz4_decode<8>, grid, dim3(kWave), lds, s, a, nb); break;
+            default: hipLaunchKernelGGL(k_lz4_decode<0>, grid, dim3(kWave), lds, s, a, nb); break;
         }
-        hipError_t e = hipGetLastError();
+        e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     uint8_t* tail_dst = out + (L.nfull * (int64_t)L.bs + L.last) * L.E;
-    hipLaunchKernelGGL(k_decode_finish, dim3(1), dim3(256), 0, s, b.status, b.offs, nb,
-                       (const int64_t*)b.idx_err, in, in_nbytes, tail_dst, tail_bytes, d_result);
+    ProfScope prof("k_decode_finish", s);
+    hipLaunchKernelGGL(k_decode_finish, dim3(1), dim3(64), 0, s, b.status, b.offs, nb,
+                       (const long long*)b.bad, (const int64_t*)b.idx_err, in, in_nbytes,
+                       tail_dst, tail_bytes, d_result);
     return hipGetLastError();
 }
 

@@ -43,20 +43,27 @@ struct EncArgs {
     Layout L;
 };
 
+// The hash table, addressed explicitly in the LDS address space: a plain
+// volatile generic pointer compiles to flat_load/flat_store sc0 sc1, whose
+// vmcnt(0) waits would drain every outstanding global load and store.
+// volatile keeps the tentative insert -> read-back order of the search.
+typedef __attribute__((address_space(3))) volatile uint16_t lds_vu16;
+typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
+
 template <bool WIDE>
 struct Table {
-    volatile uint8_t* base;
+    uint8_t* base;
     __device__ __forceinline__ uint32_t get(uint32_t h) const {
         if constexpr (WIDE)
-            return reinterpret_cast<volatile uint32_t*>(base)[h];
+            return ((lds_vu32*)base)[h];
         else
-            return reinterpret_cast<volatile uint16_t*>(base)[h];
+            return ((lds_vu16*)base)[h];
     }
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
         if constexpr (WIDE)
-            reinterpret_cast<volatile uint32_t*>(base)[h] = v;
+            ((lds_vu32*)base)[h] = v;
         else
-            reinterpret_cast<volatile uint16_t*>(base)[h] = (uint16_t)v;
+            ((lds_vu16*)base)[h] = (uint16_t)v;
     }
 };
 
@@ -250,53 +257,118 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
     return op;
 }
 
-template <int EK, bool WIDE>
-__global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x;
-    const int64_t blk = blockIdx.x;
-    const int E = EK ? EK : a.L.E;
-    const int m = blk < a.L.nfull ? a.L.bs : a.L.last;
-    const int n = m * E;
-    const int P = m / 8;
-    const uint8_t* src = a.in + blk * (int64_t)a.L.bs * E;
-    uint8_t* D = smem + kTableBytes;
+// Registers holding one 8 KiB block for EK-byte elements: 8192 / 64 lanes.
+template <int EK>
+struct BlockRegs {
+    static constexpr int kIters = EK ? 8192 / (kWave * 8 * EK) : 1;  // 64-group iterations
+    uint32_t w[kIters][2 * (EK ? EK : 1)];
+};
 
-    // zero the hash table (LZ4_initStream) and the read pad behind the block
-    for (int i = lane; i < kTableBytes / 16; i += kWave)
-        reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
-    if (lane < kDataPad / 4) reinterpret_cast<uint32_t*>(D + ((n + 3) & ~3))[lane] = 0;
+template <int EK>
+__device__ __forceinline__ void issue_block_loads(BlockRegs<EK>& R, const uint8_t* src, int P,
+                                                  int lane) {
+#pragma unroll
+    for (int it = 0; it < BlockRegs<EK>::kIters; it++) {
+        const int g = it * kWave + lane;
+        if (g < P) load_group<EK>(src + (int64_t)g * 8 * EK, R.w[it]);
+    }
+}
 
-    // bit transpose into LDS (bshuf_trans_bit_elem)
-    if constexpr (EK != 0) {
-        for (int g = lane; g < P; g += kWave) {
-            uint32_t w[2 * EK];
-            load_group<EK>(src + (int64_t)g * 8 * EK, w);
+template <int EK>
+__device__ __forceinline__ void transpose_regs_to_lds(const BlockRegs<EK>& R, uint8_t* D, int P,
+                                                      int g0, int lane) {
+#pragma unroll
+    for (int it = 0; it < BlockRegs<EK>::kIters; it++) {
+        const int g = g0 + it * kWave + lane;
+        if (g < P) {
 #pragma unroll
             for (int b = 0; b < EK; b++) {
-                const uint64_t v = tr8x8(gather_byte_plane<EK>(w, b));
+                const uint64_t v = tr8x8(gather_byte_plane<EK>(R.w[it], b));
 #pragma unroll
                 for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(v >> (8 * j));
             }
         }
-    } else {
-        for (int i = lane; i < P * E; i += kWave) {
-            const int g = i / E, b = i - g * E;
-            uint64_t v = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) v |= (uint64_t)src[(int64_t)(8 * g + k) * E + b] << (8 * k);
-            v = tr8x8(v);
-#pragma unroll
-            for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(v >> (8 * j));
-        }
     }
-    __syncthreads();
+}
 
-    uint8_t* out = a.scratch + blk * a.slot;
-    const Table<WIDE> T{smem};
-    const int c = lz4_encode_block<WIDE>(D, n, T, out + 4, lane);
-    if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
-    if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
+// Persistent: workgroup w handles blocks w, w+G, w+2G, ...  While block k is
+// parsed out of LDS, the 8 KiB of block k+G are already in flight into
+// registers, so HBM latency hides under the (LDS-latency-bound) parse.
+// One wave per workgroup: LDS hand-offs need no s_barrier, and avoiding
+// __syncthreads() keeps its release fence from draining the prefetch.
+template <int EK, bool WIDE>
+__global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x;
+    const int E = EK ? EK : a.L.E;
+    uint8_t* D = smem + kTableBytes;
+    const int64_t stride = gridDim.x;
+    int64_t blk = blockIdx.x;
+    if (blk >= nb) return;
+    auto blk_m = [&](int64_t k) { return k < a.L.nfull ? a.L.bs : a.L.last; };
+    auto blk_src = [&](int64_t k) { return a.in + k * (int64_t)a.L.bs * E; };
+
+    BlockRegs<EK> R;
+    constexpr int kRegGroups = BlockRegs<EK>::kIters * kWave;
+    // a block fits the prefetch registers when its groups fit
+    auto fits = [&](int m) { return EK != 0 && m / 8 <= kRegGroups; };
+    if constexpr (EK != 0)
+        if (fits(blk_m(blk))) issue_block_loads<EK>(R, blk_src(blk), blk_m(blk) / 8, lane);
+
+    for (;;) {
+        const int m = blk_m(blk);
+        const int n = m * E;
+        const int P = m / 8;
+        const uint8_t* src = blk_src(blk);
+        // zero the hash table (LZ4_initStream) and the read pad behind the block
+        for (int i = lane; i < kTableBytes / 16; i += kWave)
+            reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
+        if (lane < kDataPad / 4) reinterpret_cast<uint32_t*>(D + ((n + 3) & ~3))[lane] = 0;
+        // bit transpose into LDS (bshuf_trans_bit_elem)
+        if constexpr (EK != 0) {
+            if (fits(m)) {
+                transpose_regs_to_lds<EK>(R, D, P, 0, lane);
+            } else {
+                for (int g0 = 0; g0 < P; g0 += kRegGroups) {
+                    BlockRegs<EK> T;
+#pragma unroll
+                    for (int it = 0; it < BlockRegs<EK>::kIters; it++) {
+                        const int g = g0 + it * kWave + lane;
+                        if (g < P) load_group<EK>(src + (int64_t)g * 8 * EK, T.w[it]);
+                    }
+                    transpose_regs_to_lds<EK>(T, D, P, g0, lane);
+                }
+            }
+        } else {
+            for (int i = lane; i < P * E; i += kWave) {
+                const int g = i / E, b = i - g * E;
+                uint64_t v = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    v |= (uint64_t)src[(int64_t)(8 * g + k) * E + b] << (8 * k);
+                v = tr8x8(v);
+#pragma unroll
+                for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(v >> (8 * j));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // prefetch the next block while this one is parsed
+        const int64_t next = blk + stride;
+        if constexpr (EK != 0)
+            if (next < nb && fits(blk_m(next)))
+                issue_block_loads<EK>(R, blk_src(next), blk_m(next) / 8, lane);
+
+        uint8_t* out = a.scratch + blk * a.slot;
+        const Table<WIDE> T{smem};
+        const int c = lz4_encode_block<WIDE>(D, n, T, out + 4, lane);
+        if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
+        if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (next >= nb) break;
+        blk = next;
+    }
 }
 
 // Move each [BE32 c][c bytes] record from its scratch slot to out + offs[k].
@@ -354,7 +426,9 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kWave), lds, s, a);
+    const int64_t grid = persistent_grid(reinterpret_cast<const void*>(fn), kWave, lds, nb);
+    ProfScope prof("k_lz4_encode", s);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kWave), lds, s, a, nb);
     return hipGetLastError();
 }
 
@@ -424,15 +498,20 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
     e = hipMemsetAsync(b.foot + nb, 0, sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     size_t tmp = b.scan_tmp_bytes;
-    e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.foot, b.offs, (int)(nb + 1), s);
+    {
+        ProfScope prof("scan_block_offsets", s);
+        e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.foot, b.offs, (int)(nb + 1), s);
+    }
     if (e != hipSuccess) return e;
     if (nb > 0) {
+        ProfScope prof("k_compact", s);
         hipLaunchKernelGGL(k_compact, dim3((unsigned)nb), dim3(256), 0, s, b.scratch, b.slot,
                            b.offs, out);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     const uint8_t* tail_src = in + (L.nfull * (int64_t)L.bs + L.last) * L.E;
+    ProfScope prof("k_encode_finish", s);
     hipLaunchKernelGGL(k_encode_finish, dim3(1), dim3(64), 0, s, b.offs, nb, tail_src, tail_bytes,
                        out, d_result);
     return hipGetLastError();

@@ -1,0 +1,126 @@
+// prof.hip -- optional per-kernel timing with HIP events on the launch stream.
+//
+// Off by default (one relaxed flag test per launch).  When enabled with
+// bshuf_prof_enable(1), every kernel launched by the codec is bracketed by a
+// pair of events recorded on ITS stream; bshuf_prof_collect() synchronises
+// them and reports, per kernel name, the launch count and summed duration.
+// bench.py uses this to price the dominant kernel against the HBM roofline;
+// rocprofv3 --kernel-trace gives the same durations from the outside.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "launch.h"
+
+namespace bshuf {
+
+namespace {
+
+struct Rec {
+    const char* name;
+    hipEvent_t a, b;
+};
+
+struct Prof {
+    std::mutex mu;
+    bool on = false;
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+
+Prof& P() {
+    static Prof* p = new Prof();  // never destroyed: safe at process exit
+    return *p;
+}
+
+}  // namespace
+
+bool prof_on() { return P().on; }
+
+int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work) {
+    int dev = 0, cus = 256, per = 1;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess || per < 1)
+        per = 1;
+    const int64_t g = (int64_t)cus * per;
+    return work < g ? (work > 0 ? work : 1) : g;
+}
+
+ProfScope::ProfScope(const char* name, hipStream_t s) : name_(name), s_(s), a_(nullptr) {
+    Prof& p = P();
+    if (!p.on) return;
+    std::lock_guard<std::mutex> g(p.mu);
+    a_ = p.get();
+    (void)hipEventRecord((hipEvent_t)a_, s);
+}
+
+ProfScope::~ProfScope() {
+    if (!a_) return;
+    Prof& p = P();
+    std::lock_guard<std::mutex> g(p.mu);
+    hipEvent_t b = p.get();
+    (void)hipEventRecord(b, s_);
+    p.recs.push_back(Rec{name_, (hipEvent_t)a_, b});
+}
+
+}  // namespace bshuf
+
+using namespace bshuf;
+
+extern "C" {
+
+void bshuf_prof_enable(int on) {
+    Prof& p = P();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.on = on != 0;
+}
+
+// Writes "name count total_ms\n" lines into buf; returns the number of bytes
+// needed (call again with a bigger buffer if it exceeds len).  Resets.
+size_t bshuf_prof_collect(char* buf, size_t len) {
+    Prof& p = P();
+    std::lock_guard<std::mutex> g(p.mu);
+    std::map<std::string, std::pair<long, double>> acc;
+    for (auto& r : p.recs) {
+        (void)hipEventSynchronize(r.b);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, r.a, r.b);
+        auto& x = acc[r.name];
+        x.first += 1;
+        x.second += ms;
+        p.pool.push_back(r.a);
+        p.pool.push_back(r.b);
+    }
+    p.recs.clear();
+    std::string out;
+    char line[256];
+    for (auto& kv : acc) {
+        snprintf(line, sizeof line, "%s %ld %.6f\n", kv.first.c_str(), kv.second.first,
+                 kv.second.second);
+        out += line;
+    }
+    if (buf && len) {
+        const size_t n = out.size() < len - 1 ? out.size() : len - 1;
+        memcpy(buf, out.data(), n);
+        buf[n] = 0;
+    }
+    return out.size() + 1;
+}
+
+}  // extern "C"

@@ -162,6 +162,7 @@ hipError_t launch_transpose(const uint8_t* in, uint8_t* out, const Layout& L, bo
     const int64_t tiles = L.nfull * tpf + tpl;
     if (tiles == 0) return hipSuccess;
     const dim3 grid((unsigned)tiles), block(256);
+    ProfScope prof(forward ? "k_bitshuffle" : "k_bitunshuffle", s);
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
     if (aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8)) {
 #define BSHUF_T(EK)                                                                        \

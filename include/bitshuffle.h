@@ -69,6 +69,12 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
 int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first,
                              uint64_t seed, void* stream);
 
+/* Per-kernel timing (HIP events on each kernel's launch stream), for
+ * benchmarks: enable, run, then collect "name count total_ms" lines.
+ * bshuf_prof_collect returns the buffer size needed and resets. */
+void bshuf_prof_enable(int on);
+size_t bshuf_prof_collect(char* buf, size_t len);
+
 #ifdef __cplusplus
 }
 #endif
