@@ -4,7 +4,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbitshuffle_mi355x.so")
+LIB_PATH = os.environ.get("BSHUF_LIB") or os.path.join(HERE, "libbitshuffle_mi355x.so")
 PLUGIN_PATH = os.path.join(HERE, "libh5bshuf_mi355x.so")
 
 _vp = ctypes.c_void_p

@@ -33,6 +33,37 @@ namespace bshuf {
 namespace {
 
 constexpr int kTableBytes = 16384;  // byU16: 8192 x u16, byU32: 4096 x u32
+
+// Diagnostic build only (-DBSHUF_DIAG, tools/diag_encode.py): per-phase
+// s_memtime cycle sums and event counters.  The product build compiles these
+// macros to nothing.
+#ifdef BSHUF_DIAG
+__device__ unsigned long long g_diag[32];
+#define DIAG_DECL                                   \
+    uint64_t _dt = __builtin_amdgcn_s_memtime();    \
+    uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};    \
+    uint32_t _cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(i)                                       \
+    do {                                               \
+        const uint64_t _n = __builtin_amdgcn_s_memtime(); \
+        _acc[i] += _n - _dt;                           \
+        _dt = _n;                                      \
+    } while (0)
+#define COUNT(i, v) (_cnt[i] += (v))
+#define DIAG_FLUSH                                                          \
+    do {                                                                    \
+        if (lane == 0)                                                      \
+            for (int _i = 0; _i < 8; _i++) {                                \
+                atomicAdd(&g_diag[_i], (unsigned long long)_acc[_i]);       \
+                atomicAdd(&g_diag[8 + _i], (unsigned long long)_cnt[_i]);   \
+            }                                                               \
+    } while (0)
+#else
+#define DIAG_DECL
+#define STAMP(i) ((void)0)
+#define COUNT(i, v) ((void)0)
+#define DIAG_FLUSH ((void)0)
+#endif
 constexpr int kDataPad = 16;
 
 struct EncArgs {
@@ -75,64 +106,189 @@ __device__ __forceinline__ uint32_t hash_at(const uint8_t* D, int p) {
         return hash4(lds_rd32(D, p));
 }
 
-// Writes v as the LZ4 255-run continuation: v/255 bytes of 255, then v%255.
-__device__ __forceinline__ int put_len(uint8_t* out, int op, int v, int lane) {
-    const int nb = v / 255 + 1;
-    const uint8_t last = (uint8_t)(v - 255 * (nb - 1));
-    for (int i = lane; i < nb; i += kWave) out[op + i] = (i < nb - 1) ? (uint8_t)255 : last;
-    return op + nb;
+// ---------------------------------------------------------------------------
+// Output write-combining window.  Lane l holds output bytes
+// [base + 4l, base + 4l + 4) of a 256-byte window in a VGPR; tokens, length
+// bytes and offsets are bit-inserts into one lane, literals are 4-byte LDS
+// reads per lane, and a full window leaves as ONE coalesced 256-byte store.
+// (Byte-granular global stores would cost ~60x more store instructions and
+// stall the wave on its outstanding-VMEM limit.)
+// ---------------------------------------------------------------------------
+struct OutWin {
+    uint32_t w;
+    int base;  // uniform, multiple of 256
+};
+
+constexpr int kWinBytes = 4 * kWave;
+
+__device__ __forceinline__ void ow_flush(OutWin& W, uint32_t* out32, int lane) {
+    out32[(W.base >> 2) + lane] = W.w;
+    W.base += kWinBytes;
 }
 
-__device__ __forceinline__ void copy_bytes(uint8_t* out, int op, const uint8_t* D, int from,
-                                           int len, int lane) {
-    for (int i = lane; i < len; i += kWave) out[op + i] = D[from + i];
+// Byte mask of this lane's dword covering window-relative bytes [s, e).
+__device__ __forceinline__ uint32_t lane_mask(int lane, int s, int e) {
+    const int lo = 4 * lane;
+    const int a = max(s - lo, 0), b = min(e - lo, 4);
+    if (a >= b) return 0u;
+    const uint32_t hi = (b >= 4) ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    return hi & ~((1u << (8 * a)) - 1u);
 }
 
-// LZ4_count(ip, match, limit): common prefix length of D[a..] and D[b..],
-// bounded so that a + len <= lim.  64 lanes compare 4 bytes each.
-__device__ __forceinline__ int match_count(const uint8_t* D, int n, int a, int b, int lim,
-                                           int lane) {
-    int total = 0;
-    for (;;) {
-        const int pa = a + total + 4 * lane;
-        const int pb = b + total + 4 * lane;
-        const uint32_t x = lds_rd32(D, min(pa, n)) ^ lds_rd32(D, min(pb, n));
-        int eq = x ? (__ffs(x) - 1) >> 3 : 4;
-        eq = min(eq, max(lim - pa, 0));
-        const uint64_t full = ballot(eq == 4);
-        if (full == ~0ull) {
-            total += 4 * kWave;
-            continue;
+__device__ __forceinline__ void ow_byte(OutWin& W, uint32_t* out32, int& op, uint32_t b,
+                                        int lane) {
+    if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
+    const int rel = op - W.base;
+    if (lane == (rel >> 2)) {
+        const int sh = (rel & 3) * 8;
+        W.w = (W.w & ~(0xFFu << sh)) | (b << sh);
+    }
+    op++;
+}
+
+// LZ4 length continuation of v: v/255 bytes of 255, then v%255.
+__device__ __forceinline__ void ow_len(OutWin& W, uint32_t* out32, int& op, int v, int lane) {
+    int nb = v / 255 + 1;
+    const uint32_t rem = (uint32_t)(v - 255 * (nb - 1));
+    while (nb > 0) {
+        if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
+        const int rel = op - W.base;
+        const int take = min(nb, kWinBytes - rel);
+        const uint32_t m = lane_mask(lane, rel, rel + take);
+        W.w |= m;  // 0xFF bytes
+        if (take == nb) {
+            const int q = rel + take - 1;
+            if (lane == (q >> 2)) {
+                const int sh = (q & 3) * 8;
+                W.w = (W.w & ~(0xFFu << sh)) | (rem << sh);
+            }
         }
-        const int f = ffs64(~full);
-        return total + 4 * f + __builtin_amdgcn_readlane(eq, f);
+        op += take;
+        nb -= take;
     }
 }
 
-// Greedy LZ4 parse of D[0..n) with table T (zeroed), output to `out`.
-// Returns the compressed size.  Mirrors lz4/lz4.c:1002-1331 for noDict,
-// acceleration 1, notLimited output.
+// Copy D[from, from+len) (LDS) to the output stream at op.
+__device__ __forceinline__ void ow_copy(OutWin& W, uint32_t* out32, int& op, const uint8_t* D,
+                                        int from, int len, int lane) {
+    while (len > 0) {
+        if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
+        const int rel = op - W.base;
+        const int take = min(len, kWinBytes - rel);
+        const uint32_t m = lane_mask(lane, rel, rel + take);
+        const int p = from + 4 * lane - rel;  // source of this lane's first byte
+        const int pc = max(p, 0);             // p >= from - 3; lower bytes are masked
+        const uint32_t v = lds_rd32(D, pc) << (8 * (pc - p));
+        W.w = (W.w & ~m) | (v & m);
+        op += take;
+        from += take;
+        len -= take;
+    }
+}
+
+// Catch-up (lz4/lz4.c:1105-1109) and LZ4_count (lz4/lz4.c:680-703) in one
+// LDS round trip: the match bytes [ip, ip+4) are equal, so counting from
+// ip+4 does not depend on how far the catch-up goes back, and the caught-up
+// match length is back + count(ip+4).  `tail` returns the a-side dword of
+// every lane for the LAST counted 256-byte window starting at `tail_base`.
+struct CountOut {
+    int back;
+    int cnt;
+    int tail_base;
+    uint32_t tail;
+};
+
+__device__ __forceinline__ CountOut catch_and_count(const uint8_t* D, int n, int ip, int ref,
+                                                    int anchor, int mlimit, int lane) {
+    CountOut r;
+    // first forward window and backward bytes together
+    const int a = ip + kMinMatch, b = ref + kMinMatch;
+    int pa = a + 4 * lane, pb = b + 4 * lane;
+    uint32_t va = lds_rd32(D, min(pa, n)), vb = lds_rd32(D, min(pb, n));
+    const int ba = ip - 1 - lane, bb = ref - 1 - lane;
+    const uint32_t ca = D[max(ba, 0)], cb = D[max(bb, 0)];
+    // backward
+    {
+        uint64_t cm = ballot(ba >= anchor && bb >= 0 && ca == cb);
+        int back = (~cm) ? ffs64(~cm) : kWave;
+        if (back == kWave) {
+            for (int base = kWave;; base += kWave) {
+                const int xa = ip - 1 - base - lane, xb = ref - 1 - base - lane;
+                cm = ballot(xa >= anchor && xb >= 0 && D[max(xa, 0)] == D[max(xb, 0)]);
+                const int run = (~cm) ? ffs64(~cm) : kWave;
+                back = base + run;
+                if (run < kWave) break;
+            }
+        }
+        r.back = back;
+    }
+    // forward
+    int total = 0;
+    for (;;) {
+        const uint32_t x = va ^ vb;
+        int eq = x ? (__ffs(x) - 1) >> 3 : 4;
+        eq = min(eq, max(mlimit - pa, 0));
+        const uint64_t full = ballot(eq == 4);
+        if (full != ~0ull) {
+            const int f = ffs64(~full);
+            r.cnt = total + 4 * f + __builtin_amdgcn_readlane(eq, f);
+            r.tail_base = a + total;
+            r.tail = va;
+            return r;
+        }
+        total += kWinBytes;
+        pa = a + total + 4 * lane;
+        pb = b + total + 4 * lane;
+        va = lds_rd32(D, min(pa, n));
+        vb = lds_rd32(D, min(pb, n));
+    }
+}
+
+// read32 at position p from the a-side window registers (p - base in
+// [0, 252]), without an LDS round trip.
+__device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
+    const int t = p - base;
+    const int l = t >> 2;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, min(l + 1, kWave - 1));
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(t & 3));
+}
+
+// Greedy LZ4 parse of D[0..n) with table T (zeroed); compressed bytes go to
+// out32 (4-byte aligned, room for the bound rounded up to 256).  Returns the
+// compressed size.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1,
+// notLimited output.
 template <bool WIDE>
-__device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE> T, uint8_t* out,
-                                const int lane) {
+__device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE> T,
+                                uint32_t* out32, const int lane) {
+    DIAG_DECL
+    OutWin W{0u, 0};
     int op = 0, anchor = 0;
     if (n >= kLz4MinLength) {
         const int limit = n - kMfLimit + 1;  // mflimitPlusOne
         const int mlimit = n - kLastLiterals;
         int ip = 1;  // position 0 is pre-inserted: a zeroed table already says 0
+        // sequence of the first probe window, issued ahead of need
+        uint32_t pre = lds_rd32(D, min(ip + lane, n));
         for (;;) {
             // ------------------------------------------------ search
             int mpos = -1, mref = 0;
             {
                 const int p0 = ip;
+                COUNT(6, 1);
+                uint32_t seq_cur = pre;  // valid for k0 == 0 (positions p0 + lane)
                 for (int k0 = 0;; k0 += kWave) {
+                    COUNT(1, 1);
                     const int pos = p0 + probe_offset(k0 + lane);
                     const bool valid = p0 + probe_offset(k0 + lane + 1) <= limit;
                     const uint64_t vmask = ballot(valid);
                     if (vmask == 0) break;
-                    uint32_t seq = 0, h = 0, cold = 0;
+                    // next window's sequences, in flight while this one resolves
+                    const int pos_n = p0 + probe_offset(k0 + kWave + lane);
+                    const uint32_t seq_nxt = lds_rd32(D, min(pos_n, n));
+                    const uint32_t seq = seq_cur;
+                    uint32_t h = 0, cold = 0;
                     if (valid) {
-                        seq = lds_rd32(D, pos);
                         if constexpr (WIDE)
                             h = hash5(lds_rd64(D, pos));
                         else
@@ -141,11 +297,14 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
                     }
                     if (valid) T.put(h, (uint32_t)pos);
                     const uint32_t rb = valid ? T.get(h) : (uint32_t)pos;
+                    const uint32_t dcold = lds_rd32(D, (int)cold);
                     const bool loser = valid && rb != (uint32_t)pos;
                     uint32_t cand = cold;
+                    int pred = -1;
                     bool grouped = false, first = true;
                     int next_member = kWave;
                     uint64_t lmask = ballot(loser);
+                    COUNT(2, lmask ? 1 : 0);
                     while (lmask) {
                         const int l = ffs64(lmask);
                         const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, l);
@@ -155,7 +314,8 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
                             grouped = true;
                             const uint64_t below = g & ((1ull << lane) - 1ull);
                             if (below) {
-                                cand = (uint32_t)(p0 + probe_offset(k0 + fls64(below)));
+                                pred = fls64(below);
+                                cand = (uint32_t)(p0 + probe_offset(k0 + pred));
                                 first = false;
                             }
                             const uint64_t above = lane == 63 ? 0ull : (g & (~0ull << (lane + 1)));
@@ -163,10 +323,13 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
                         }
                         lmask &= ~g;
                     }
+                    // candidate bytes: the table's position, or the in-window predecessor's
+                    const uint32_t dpred = (uint32_t)__shfl((int)seq, pred < 0 ? lane : pred);
+                    const uint32_t dcand = pred < 0 ? dcold : dpred;
                     bool ok = false;
                     if (valid) {
                         const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
-                        ok = near && lds_rd32(D, (int)cand) == seq;
+                        ok = near && dcand == seq;
                     }
                     const uint64_t mm = ballot(ok);
                     if (mm) {
@@ -186,59 +349,67 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
                     }
                     if (vmask != ~0ull) break;  // ran past mflimit: last literals
                     if (grouped && next_member == kWave) T.put(h, (uint32_t)pos);
+                    seq_cur = seq_nxt;
                 }
             }
+            STAMP(0);
             if (mpos < 0) break;
-            ip = mpos;
-            int ref = mref;
-            // ------------------------------------------------ catch up
-            for (;;) {
-                const int a = ip - 1 - lane, b = ref - 1 - lane;
-                const bool c = a >= anchor && b >= 0 && D[max(a, 0)] == D[max(b, 0)];
-                const uint64_t cm = ballot(c);
-                const int run = (~cm) ? ffs64(~cm) : kWave;
-                ip -= run;
-                ref -= run;
-                if (run < kWave) break;
-            }
-            // ------------------------------------------------ literals
-            int tokpos = op++;
-            int tok;
+            COUNT(0, 1);
+            // ------------------------------------------------ catch up + count
+            CountOut co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
+            ip = mpos - co.back;
+            int ref = mref - co.back;
+            int mc = co.back + co.cnt;
+            STAMP(1);
+            // ------------------------------------------------ emit sequence
             {
                 const int lit = ip - anchor;
-                tok = (lit >= 15 ? 15 : lit) << 4;
-                if (lit >= 15) op = put_len(out, op, lit - 15, lane);
-                copy_bytes(out, op, D, anchor, lit, lane);
-                op += lit;
+                ow_byte(W, out32, op, (uint32_t)(((lit >= 15 ? 15 : lit) << 4) | (mc >= 15 ? 15 : mc)),
+                        lane);
+                if (lit >= 15) ow_len(W, out32, op, lit - 15, lane);
+                ow_copy(W, out32, op, D, anchor, lit, lane);
+                COUNT(5, lit);
             }
-            // ------------------------------------------------ matches
+            STAMP(2);
             for (;;) {
                 const int off = ip - ref;
-                if (lane == 0) {
-                    out[op] = (uint8_t)off;
-                    out[op + 1] = (uint8_t)(off >> 8);
-                }
-                op += 2;
-                const int mc = match_count(D, n, ip + kMinMatch, ref + kMinMatch, mlimit, lane);
+                ow_byte(W, out32, op, (uint32_t)(off & 0xFF), lane);
+                ow_byte(W, out32, op, (uint32_t)(off >> 8), lane);
+                if (mc >= 15) ow_len(W, out32, op, mc - 15, lane);
                 ip += mc + kMinMatch;
-                tok |= mc >= 15 ? 15 : mc;
-                if (lane == 0) out[tokpos] = (uint8_t)tok;
-                if (mc >= 15) op = put_len(out, op, mc - 15, lane);
                 anchor = ip;
+                STAMP(3);
                 if (ip >= limit) break;
                 // fill table at ip-2, then test ip (lz4/lz4.c:1230-1293)
-                const uint32_t h2 = hash_at<WIDE>(D, ip - 2);
-                const uint32_t h0 = hash_at<WIDE>(D, ip);
+                const int t = ip - co.tail_base;
+                uint32_t x2, x0, h2, h0;
+                if (!WIDE && t >= 2 && t <= 4 * kWave - 8) {
+                    x2 = win_rd32(co.tail, co.tail_base, ip - 2);
+                    x0 = win_rd32(co.tail, co.tail_base, ip);
+                    h2 = hash4(x2);
+                    h0 = hash4(x0);
+                } else {
+                    x0 = lds_rd32(D, ip);
+                    h2 = hash_at<WIDE>(D, ip - 2);
+                    h0 = hash_at<WIDE>(D, ip);
+                }
+                // the next search window's bytes, in flight during the re-test
+                pre = lds_rd32(D, min(ip + 1 + lane, n));
                 if (lane == 0) T.put(h2, (uint32_t)(ip - 2));
                 const uint32_t c2 = uni(T.get(h0));
                 if (lane == 0) T.put(h0, (uint32_t)ip);
                 const bool near = !WIDE || c2 + kMaxDistance >= (uint32_t)ip;
-                if (near && lds_rd32(D, (int)c2) == lds_rd32(D, ip)) {
-                    tokpos = op++;
-                    tok = 0;
+                if (near && lds_rd32(D, (int)c2) == x0) {
+                    // zero-literal sequence, no catch-up on this path
                     ref = (int)c2;
+                    co = catch_and_count(D, n, ip, ref, ip, mlimit, lane);
+                    mc = co.cnt;  // back == 0: anchor == ip
+                    ow_byte(W, out32, op, (uint32_t)(mc >= 15 ? 15 : mc), lane);
+                    COUNT(3, 1);
+                    STAMP(4);
                     continue;
                 }
+                STAMP(4);
                 break;
             }
             if (anchor >= limit) break;
@@ -248,12 +419,14 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
     // ---------------------------------------------------- last literals
     {
         const int run = n - anchor;
-        if (lane == 0) out[op] = (uint8_t)((run >= 15 ? 15 : run) << 4);
-        op++;
-        if (run >= 15) op = put_len(out, op, run - 15, lane);
-        copy_bytes(out, op, D, anchor, run, lane);
-        op += run;
+        ow_byte(W, out32, op, (uint32_t)((run >= 15 ? 15 : run) << 4), lane);
+        if (run >= 15) ow_len(W, out32, op, run - 15, lane);
+        ow_copy(W, out32, op, D, anchor, run, lane);
     }
+    if (op > W.base) ow_flush(W, out32, lane);
+    STAMP(5);
+    COUNT(4, 1);
+    DIAG_FLUSH;
     return op;
 }
 
@@ -361,7 +534,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 
         uint8_t* out = a.scratch + blk * a.slot;
         const Table<WIDE> T{smem};
-        const int c = lz4_encode_block<WIDE>(D, n, T, out + 4, lane);
+        const int c = lz4_encode_block<WIDE>(D, n, T, reinterpret_cast<uint32_t*>(out + 4), lane);
         if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -438,8 +611,10 @@ int64_t max_device_block_bytes() { return 160 * 1024 - kTableBytes - 64; }
 
 int64_t encode_slot_bytes(const Layout& L) {
     const int64_t n = (int64_t)L.bs * L.E;
-    // header + bound + 16 for the 5-dword over-read in k_compact, 16-aligned
-    return ((4 + (int64_t)lz4_bound((int)n) + 16) + 15) & ~(int64_t)15;
+    // header + bound rounded up to the 256-byte output window (the encoder
+    // flushes whole windows) + 16 for k_compact's 5-dword over-read, 16-aligned
+    const int64_t payload = ((int64_t)lz4_bound((int)n) + 255) & ~(int64_t)255;
+    return (4 + payload + 16 + 15) & ~(int64_t)15;
 }
 
 size_t encode_scan_tmp_bytes(int64_t nblocks) {
@@ -518,3 +693,14 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
 }
 
 }  // namespace bshuf
+
+#ifdef BSHUF_DIAG
+// Diagnostic build only: read (and reset) the encoder's phase counters.
+extern "C" int bshuf_diag_read(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bshuf::g_diag), sizeof(unsigned long long) * 32) !=
+        hipSuccess)
+        return -1;
+    unsigned long long z[32] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(bshuf::g_diag), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif

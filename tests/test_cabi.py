@@ -42,7 +42,7 @@ def test_library_exports_every_declared_symbol():
     missing = sorted(want - exported)
     assert not missing, missing
     # the ctypes prototype table covers the whole core ABI
-    core = {n for n in want if n.startswith("bshuf_") and "h5" not in n}
+    core = {n for n in want if n.startswith("bshuf_") and "h5" not in n.lower()}
     assert core <= set(PROTOTYPES), sorted(core - set(PROTOTYPES))
 
 
