@@ -22,6 +22,9 @@ class ProfScope {
     void* a_;
 };
 
+// Kernel-variant knob for A/B measurements (bshuf_set_variant); 0 = default.
+int tuning_variant();
+
 // Workgroups for a persistent launch: resident blocks per CU (occupancy API,
 // dynamic LDS included) x CUs of the current device, capped by the work.
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work);

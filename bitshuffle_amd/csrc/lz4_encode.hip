@@ -186,6 +186,42 @@ __device__ __forceinline__ void ow_copy(OutWin& W, uint32_t* out32, int& op, con
     }
 }
 
+// Emission policies for lz4_encode_block: EmitWin (register window, one
+// coalesced store per 256 bytes) and EmitBytes (byte-granular stores).
+struct EmitWin {
+    OutWin W{0u, 0};
+    uint32_t* out32;
+    int lane;
+    __device__ __forceinline__ void byte(int& op, uint32_t b) { ow_byte(W, out32, op, b, lane); }
+    __device__ __forceinline__ void len(int& op, int v) { ow_len(W, out32, op, v, lane); }
+    __device__ __forceinline__ void copy(int& op, const uint8_t* D, int from, int n) {
+        ow_copy(W, out32, op, D, from, n, lane);
+    }
+    __device__ __forceinline__ void finish(int op) {
+        if (op > W.base) ow_flush(W, out32, lane);
+    }
+};
+
+struct EmitBytes {
+    uint8_t* out;
+    int lane;
+    __device__ __forceinline__ void byte(int& op, uint32_t b) {
+        if (lane == 0) out[op] = (uint8_t)b;
+        op++;
+    }
+    __device__ __forceinline__ void len(int& op, int v) {
+        const int nb = v / 255 + 1;
+        const uint8_t last = (uint8_t)(v - 255 * (nb - 1));
+        for (int i = lane; i < nb; i += kWave) out[op + i] = (i < nb - 1) ? (uint8_t)255 : last;
+        op += nb;
+    }
+    __device__ __forceinline__ void copy(int& op, const uint8_t* D, int from, int n) {
+        for (int i = lane; i < n; i += kWave) out[op + i] = D[from + i];
+        op += n;
+    }
+    __device__ __forceinline__ void finish(int) {}
+};
+
 // Catch-up (lz4/lz4.c:1105-1109) and LZ4_count (lz4/lz4.c:680-703) in one
 // LDS round trip: the match bytes [ip, ip+4) are equal, so counting from
 // ip+4 does not depend on how far the catch-up goes back, and the caught-up
@@ -258,11 +294,10 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
 // out32 (4-byte aligned, room for the bound rounded up to 256).  Returns the
 // compressed size.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1,
 // notLimited output.
-template <bool WIDE>
-__device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE> T,
-                                uint32_t* out32, const int lane) {
+template <bool WIDE, class Emit>
+__device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE> T, Emit& em,
+                                const int lane) {
     DIAG_DECL
-    OutWin W{0u, 0};
     int op = 0, anchor = 0;
     if (n >= kLz4MinLength) {
         const int limit = n - kMfLimit + 1;  // mflimitPlusOne
@@ -364,18 +399,17 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
             // ------------------------------------------------ emit sequence
             {
                 const int lit = ip - anchor;
-                ow_byte(W, out32, op, (uint32_t)(((lit >= 15 ? 15 : lit) << 4) | (mc >= 15 ? 15 : mc)),
-                        lane);
-                if (lit >= 15) ow_len(W, out32, op, lit - 15, lane);
-                ow_copy(W, out32, op, D, anchor, lit, lane);
+                em.byte(op, (uint32_t)(((lit >= 15 ? 15 : lit) << 4) | (mc >= 15 ? 15 : mc)));
+                if (lit >= 15) em.len(op, lit - 15);
+                em.copy(op, D, anchor, lit);
                 COUNT(5, lit);
             }
             STAMP(2);
             for (;;) {
                 const int off = ip - ref;
-                ow_byte(W, out32, op, (uint32_t)(off & 0xFF), lane);
-                ow_byte(W, out32, op, (uint32_t)(off >> 8), lane);
-                if (mc >= 15) ow_len(W, out32, op, mc - 15, lane);
+                em.byte(op, (uint32_t)(off & 0xFF));
+                em.byte(op, (uint32_t)(off >> 8));
+                if (mc >= 15) em.len(op, mc - 15);
                 ip += mc + kMinMatch;
                 anchor = ip;
                 STAMP(3);
@@ -404,7 +438,7 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
                     ref = (int)c2;
                     co = catch_and_count(D, n, ip, ref, ip, mlimit, lane);
                     mc = co.cnt;  // back == 0: anchor == ip
-                    ow_byte(W, out32, op, (uint32_t)(mc >= 15 ? 15 : mc), lane);
+                    em.byte(op, (uint32_t)(mc >= 15 ? 15 : mc));
                     COUNT(3, 1);
                     STAMP(4);
                     continue;
@@ -419,11 +453,11 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
     // ---------------------------------------------------- last literals
     {
         const int run = n - anchor;
-        ow_byte(W, out32, op, (uint32_t)((run >= 15 ? 15 : run) << 4), lane);
-        if (run >= 15) ow_len(W, out32, op, run - 15, lane);
-        ow_copy(W, out32, op, D, anchor, run, lane);
+        em.byte(op, (uint32_t)((run >= 15 ? 15 : run) << 4));
+        if (run >= 15) em.len(op, run - 15);
+        em.copy(op, D, anchor, run);
     }
-    if (op > W.base) ow_flush(W, out32, lane);
+    em.finish(op);
     STAMP(5);
     COUNT(4, 1);
     DIAG_FLUSH;
@@ -469,7 +503,7 @@ __device__ __forceinline__ void transpose_regs_to_lds(const BlockRegs<EK>& R, ui
 // registers, so HBM latency hides under the (LDS-latency-bound) parse.
 // One wave per workgroup: LDS hand-offs need no s_barrier, and avoiding
 // __syncthreads() keeps its release fence from draining the prefetch.
-template <int EK, bool WIDE>
+template <int EK, bool WIDE, int VAR>
 __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
@@ -534,7 +568,18 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 
         uint8_t* out = a.scratch + blk * a.slot;
         const Table<WIDE> T{smem};
-        const int c = lz4_encode_block<WIDE>(D, n, T, reinterpret_cast<uint32_t*>(out + 4), lane);
+        int c;
+        if constexpr (VAR == 0) {
+            // default: byte-granular stores measured 11% faster than the
+            // register window (tools/ab.py, 2 GiB G1: 9.13 vs 10.29 ms)
+            EmitBytes em{out + 4, lane};
+            c = lz4_encode_block<WIDE>(D, n, T, em, lane);
+        } else {
+            EmitWin em;
+            em.out32 = reinterpret_cast<uint32_t*>(out + 4);
+            em.lane = lane;
+            c = lz4_encode_block<WIDE>(D, n, T, em, lane);
+        }
         if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -591,9 +636,11 @@ __global__ void k_encode_finish(const uint64_t* offs, int64_t nblocks, const uin
     if (threadIdx.x == 0) *result = (int64_t)end + tail;
 }
 
-template <int EK, bool WIDE>
+template <int EK, bool WIDE, int VAR = 0>
 hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s) {
-    auto fn = k_lz4_encode<EK, WIDE>;
+    if constexpr (EK == 2 && !WIDE && VAR == 0)
+        if (tuning_variant() == 1) return launch_enc_t<2, false, 1>(a, nb, lds, s);  // window
+    auto fn = k_lz4_encode<EK, WIDE, VAR>;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -52,6 +52,9 @@ Prof& P() {
 
 bool prof_on() { return P().on; }
 
+static int g_variant = 0;
+int tuning_variant() { return g_variant; }
+
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work) {
     int dev = 0, cus = 256, per = 1;
     if (hipGetDevice(&dev) == hipSuccess)
@@ -84,6 +87,8 @@ ProfScope::~ProfScope() {
 using namespace bshuf;
 
 extern "C" {
+
+void bshuf_set_variant(int v) { g_variant = v; }
 
 void bshuf_prof_enable(int on) {
     Prof& p = P();
