@@ -53,7 +53,8 @@ __device__ int64_t chase(const uint8_t* in, int64_t p, int64_t stop, int64_t Cb,
 __global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in, int64_t Cb,
                                                   int64_t CH, int64_t W, uint32_t maxlen,
                                                   int64_t* __restrict__ exits) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kIdxWinMax + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kIdxWinMax + 48];
+    int win_off = 0;
     const int lane = threadIdx.x;
     const int64_t s = blockIdx.x;
     const int64_t cs = s * CH;
@@ -62,15 +63,24 @@ __global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in
     const int64_t wbytes = min(cend + 3, Cb) - cs;
     const bool use_lds = wbytes <= kIdxWinMax;
     if (use_lds) {
-        for (int64_t i = lane; i < wbytes; i += kWave) win[i] = in[cs + i];
+        // 16-byte loads of the candidate window, aligned on the ABSOLUTE
+        // address: an aligned granule never crosses a page, so the bytes it
+        // reads outside [cs, cs+wbytes) cannot fault and are never used
+        const uintptr_t start = (uintptr_t)(in + cs);
+        const uint4* g4 = reinterpret_cast<const uint4*>(start & ~(uintptr_t)15);
+        const int sh = (int)(start & 15);
+        const int nch = (sh + (int)wbytes + 15) >> 4;
+        uint4* w4 = reinterpret_cast<uint4*>(win);
+        for (int c = lane; c < nch; c += kWave) w4[c] = g4[c];
         __syncthreads();
+        win_off = sh;
     }
     int64_t lo = INT64_MAX, hi = -1;
     for (int64_t c = cs + lane; c < cend; c += kWave) {
         if (c + 4 > Cb) continue;
         uint32_t len;
         if (use_lds) {
-            const uint8_t* q = win + (c - cs);
+            const uint8_t* q = win + win_off + (c - cs);
             len = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
         } else {
             len = be32_global(in + c);
@@ -278,34 +288,36 @@ struct PayRegs {
     uint4 v[kPayIters];
 };
 
-__device__ __forceinline__ bool span_fits(const Span& sp) {
-    const int64_t a0 = sp.o0 & ~(int64_t)15;
-    return ((sp.o1 - a0 + 15) >> 4) <= kPayIters * kWave;
+// Record bytes [o0, o1) are read as whole 16-byte granules aligned on the
+// absolute address (a granule never crosses a page: the extra bytes at either
+// end cannot fault and are never used); they land in LDS at Cbuf + (addr & 15).
+__device__ __forceinline__ const uint4* span_base(const DecArgs& a, const Span& sp) {
+    return reinterpret_cast<const uint4*>((uintptr_t)(a.in + sp.o0) & ~(uintptr_t)15);
+}
+__device__ __forceinline__ int span_shift(const DecArgs& a, const Span& sp) {
+    return (int)((uintptr_t)(a.in + sp.o0) & 15);
+}
+__device__ __forceinline__ int span_chunks(const DecArgs& a, const Span& sp) {
+    return (span_shift(a, sp) + (int)(sp.o1 - sp.o0) + 15) >> 4;
 }
 
-// Loads the 16-byte-aligned chunks covering [o0, o1); chunks that reach past
-// in_nbytes are assembled bytewise so nothing is read outside the stream.
-__device__ __forceinline__ uint4 load_chunk(const uint8_t* in, int64_t in_nbytes, int64_t gb) {
-    if (gb + 16 <= in_nbytes) return *reinterpret_cast<const uint4*>(in + gb);
-    uint32_t w[4] = {0, 0, 0, 0};
-    for (int j = 0; j < 16; j++)
-        if (gb + j < in_nbytes) w[j >> 2] |= (uint32_t)in[gb + j] << (8 * (j & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
+__device__ __forceinline__ bool span_fits(const DecArgs& a, const Span& sp) {
+    return span_chunks(a, sp) <= kPayIters * kWave;
 }
 
 __device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Span& sp, int lane) {
-    const int64_t a0 = sp.o0 & ~(int64_t)15;
-    const int nch = (int)((sp.o1 - a0 + 15) >> 4);
+    const uint4* g4 = span_base(a, sp);
+    const int nch = span_chunks(a, sp);
 #pragma unroll
     for (int it = 0; it < kPayIters; it++) {
         const int c = it * kWave + lane;
-        if (c < nch) R.v[it] = load_chunk(a.in, a.in_nbytes, a0 + 16 * (int64_t)c);
+        if (c < nch) R.v[it] = g4[c];
     }
 }
 
-__device__ __forceinline__ void land_pay(const PayRegs& R, const Span& sp, uint8_t* C, int lane) {
-    const int64_t a0 = sp.o0 & ~(int64_t)15;
-    const int nch = (int)((sp.o1 - a0 + 15) >> 4);
+__device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, const Span& sp,
+                                         uint8_t* C, int lane) {
+    const int nch = span_chunks(a, sp);
 #pragma unroll
     for (int it = 0; it < kPayIters; it++) {
         const int c = it * kWave + lane;
@@ -331,7 +343,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     Span nxt = {0, 0};
     if (blk + stride < nb) nxt = span_of(a, blk + stride, nb);
     PayRegs R;
-    bool cur_in_regs = span_fits(cur);
+    bool cur_in_regs = span_fits(a, cur);
     if (cur_in_regs) issue_pay(R, a, cur, lane);
 
     for (;;) {
@@ -340,23 +352,22 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         const int P = m / 8;
         // land this record in LDS
         if (cur_in_regs) {
-            land_pay(R, cur, Cbuf, lane);
+            land_pay(R, a, cur, Cbuf, lane);
         } else {
-            const int64_t a0 = cur.o0 & ~(int64_t)15;
-            const int nch = (int)((cur.o1 - a0 + 15) >> 4);
-            for (int c = lane; c < nch; c += kWave)
-                reinterpret_cast<uint4*>(Cbuf)[c] = load_chunk(a.in, a.in_nbytes, a0 + 16 * (int64_t)c);
+            const uint4* g4 = span_base(a, cur);
+            const int nch = span_chunks(a, cur);
+            for (int c = lane; c < nch; c += kWave) reinterpret_cast<uint4*>(Cbuf)[c] = g4[c];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // prefetch: next record into registers, the one after into `nxt2`
         const int64_t next = blk + stride;
-        const bool next_in_regs = next < nb && span_fits(nxt);
+        const bool next_in_regs = next < nb && span_fits(a, nxt);
         if (next_in_regs) issue_pay(R, a, nxt, lane);
         Span nxt2 = {0, 0};
         if (next + stride < nb) nxt2 = span_of(a, next + stride, nb);
 
-        const uint8_t* C = Cbuf + (cur.o0 & 15);
+        const uint8_t* C = Cbuf + span_shift(a, cur);
         const int avail = (int)(cur.o1 - cur.o0);
         int status = 0, clen = 0;
         if (avail < 4) {

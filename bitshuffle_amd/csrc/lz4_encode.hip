@@ -597,15 +597,16 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
                                                  const uint64_t* __restrict__ offs,
                                                  uint8_t* __restrict__ out) {
     const int64_t blk = blockIdx.x;
-    const uint64_t dst0 = offs[blk];
-    const int64_t len = (int64_t)(offs[blk + 1] - dst0);
+    const uint64_t rel0 = offs[blk];
+    const int64_t len = (int64_t)(offs[blk + 1] - rel0);
     const uint8_t* rec = scratch + blk * slot;
     const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(rec);
-    const int64_t q0 = (int64_t)(dst0 >> 4);
-    const int64_t q1 = (int64_t)((dst0 + len + 15) >> 4);
-    for (int64_t q = q0 + threadIdx.x; q < q1; q += 256) {
-        const int64_t d = q * 16;
-        const int64_t s = d - (int64_t)dst0;  // record offset of this chunk's first byte
+    // 16-byte chunks of the ABSOLUTE destination address space
+    const uintptr_t dst0 = (uintptr_t)(out + rel0);
+    const uintptr_t q0 = dst0 >> 4, q1 = (dst0 + (uintptr_t)len + 15) >> 4;
+    for (uintptr_t q = q0 + threadIdx.x; q < q1; q += 256) {
+        const int64_t s = (int64_t)(q * 16 - dst0);  // record offset of the chunk's first byte
+        uint8_t* d = reinterpret_cast<uint8_t*>(q * 16);
         if (s >= 0 && s + 16 <= len) {
             const int64_t w0 = s >> 2;
             const uint32_t sh = (uint32_t)(s & 3);
@@ -617,11 +618,11 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
             v.y = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
             v.z = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
             v.w = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
-            *reinterpret_cast<uint4*>(out + d) = v;
+            *reinterpret_cast<uint4*>(d) = v;
         } else {
             for (int i = 0; i < 16; i++) {
                 const int64_t r = s + i;
-                if (r >= 0 && r < len) out[d + i] = rec[r];
+                if (r >= 0 && r < len) d[i] = rec[r];
             }
         }
     }

@@ -232,3 +232,36 @@ def test_full_size_digests(bs, torch):
         assert torch.equal(d, x), name
         del x, c, d
         torch.cuda.empty_cache()
+
+
+def test_device_api_unaligned_pointers(bs, oracle, torch):
+    """Device entry points on pointers that are NOT 16-byte aligned (odd
+    offsets into larger allocations) give the same bytes."""
+    import ctypes
+    a = oracle.gen_g1(3 * 4096 + 517)
+    want = oracle.compress_lz4(a)
+    nbytes = a.nbytes
+    for off_in, off_out in [(1, 3), (7, 0), (0, 5), (2, 2)]:
+        src = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
+        src[off_in:off_in + nbytes] = torch.from_numpy(a.view(np.uint8).copy()).cuda()
+        bound = bs.compress_lz4_bound(a.size, 2)
+        dst = torch.zeros(bound + 64, dtype=torch.uint8, device="cuda")
+        res = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rc = bs.lib.bshuf_compress_lz4_dev(ctypes.c_void_p(src.data_ptr() + off_in),
+                                           ctypes.c_void_p(dst.data_ptr() + off_out), a.size, 2, 0,
+                                           None, 0, ctypes.c_void_p(res.data_ptr()), None, None)
+        assert rc == 0
+        n = int(res.item())
+        assert dst[off_out:off_out + n].cpu().numpy().tobytes() == want.tobytes(), (off_in, off_out)
+        back = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
+        rc = bs.lib.bshuf_decompress_lz4_dev(ctypes.c_void_p(dst.data_ptr() + off_out), n,
+                                             ctypes.c_void_p(back.data_ptr() + off_in), a.size, 2,
+                                             0, None, 0, ctypes.c_void_p(res.data_ptr()), None, None)
+        assert rc == 0 and int(res.item()) == n
+        assert back[off_in:off_in + nbytes].cpu().numpy().tobytes() == a.view(np.uint8).tobytes()
+        sh = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
+        r = bs.lib.bshuf_bitshuffle_dev(ctypes.c_void_p(src.data_ptr() + off_in),
+                                        ctypes.c_void_p(sh.data_ptr() + off_out), a.size, 2, 0, None)
+        torch.cuda.synchronize()
+        assert r == nbytes
+        assert sh[off_out:off_out + nbytes].cpu().numpy().tobytes() == oracle.bitshuffle(a).tobytes()
