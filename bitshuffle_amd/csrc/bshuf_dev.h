@@ -75,6 +75,41 @@ __device__ __forceinline__ uint32_t hash5(uint64_t seq) {
     return (uint32_t)(((seq << 24) * 889523592379ull) >> 52);
 }
 
+// LDS-typed pointers (address space 3): 32-bit offsets, constant parts folded
+// into the DS instruction's immediate offset.  Generic pointers to __shared__
+// data compile to 64-bit address math plus a conversion per access.
+typedef __attribute__((address_space(3))) uint8_t lds8;
+typedef __attribute__((address_space(3))) uint16_t lds16;
+typedef __attribute__((address_space(3))) uint32_t lds32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds128;
+__device__ __forceinline__ u32x4 vec4(const uint4& v) { return u32x4{v.x, v.y, v.z, v.w}; }
+
+__device__ __forceinline__ lds8* to_lds(void* p) { return (lds8*)(p); }
+
+// Global (address space 1) pointers for loads/stores whose address went
+// through integer arithmetic: without the cast they compile to flat_* ops,
+// which also count on lgkmcnt and so make every LDS wait drain them.
+typedef __attribute__((address_space(1))) const u32x4 gbl128c;
+typedef __attribute__((address_space(1))) u32x4 gbl128;
+typedef __attribute__((address_space(1))) uint8_t gbl8;
+__device__ __forceinline__ const gbl128c* g128_aligned_down(const void* p) {
+    return (const gbl128c*)((uintptr_t)p & ~(uintptr_t)15);
+}
+
+__device__ __forceinline__ uint32_t lds_rd32(const lds8* D, int p) {
+    const lds32* w = (const lds32*)(D + (p & ~3));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(p & 3));
+}
+
+__device__ __forceinline__ uint64_t lds_rd64(const lds8* D, int p) {
+    const lds32* w = (const lds32*)(D + (p & ~3));
+    const uint32_t s = (uint32_t)(p & 3);
+    const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], s);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(w[2], w[1], s);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 // Unaligned little-endian loads from LDS: two aligned dwords + v_alignbyte.
 __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* D, int p) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(D + (p & ~3));

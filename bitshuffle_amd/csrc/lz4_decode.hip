@@ -53,7 +53,7 @@ __device__ int64_t chase(const uint8_t* in, int64_t p, int64_t stop, int64_t Cb,
 __global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in, int64_t Cb,
                                                   int64_t CH, int64_t W, uint32_t maxlen,
                                                   int64_t* __restrict__ exits) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kIdxWinMax + 48];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kIdxWinMax + 64];
     int win_off = 0;
     const int lane = threadIdx.x;
     const int64_t s = blockIdx.x;
@@ -67,29 +67,39 @@ __global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in
         // address: an aligned granule never crosses a page, so the bytes it
         // reads outside [cs, cs+wbytes) cannot fault and are never used
         const uintptr_t start = (uintptr_t)(in + cs);
-        const uint4* g4 = reinterpret_cast<const uint4*>(start & ~(uintptr_t)15);
+        const gbl128c* g4 = g128_aligned_down(in + cs);
         const int sh = (int)(start & 15);
         const int nch = (sh + (int)wbytes + 15) >> 4;
-        uint4* w4 = reinterpret_cast<uint4*>(win);
+        lds128* w4 = (lds128*)to_lds(win);
         for (int c = lane; c < nch; c += kWave) w4[c] = g4[c];
         __syncthreads();
         win_off = sh;
     }
     int64_t lo = INT64_MAX, hi = -1;
-    for (int64_t c = cs + lane; c < cend; c += kWave) {
-        if (c + 4 > Cb) continue;
-        uint32_t len;
-        if (use_lds) {
-            const uint8_t* q = win + win_off + (c - cs);
-            len = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-        } else {
-            len = be32_global(in + c);
-        }
-        if (len == 0 || len > maxlen || c + 4 + (int64_t)len > Cb) continue;
+    auto try_cand = [&](int64_t c, uint32_t len) {
+        if (c >= cend || c + 4 > Cb) return;
+        if (len == 0 || len > maxlen || c + 4 + (int64_t)len > Cb) return;
         const int64_t x = chase(in, c + 4 + len, ce, Cb, maxlen);
-        if (x == kDead) continue;
+        if (x == kDead) return;
         lo = min(lo, x);
         hi = max(hi, x);
+    };
+    if (use_lds) {
+        // 4 consecutive candidates per lane: two dword reads cover the 7
+        // bytes of their four big-endian length words
+        const lds8* wq = (const lds8*)to_lds(win) + win_off;
+        for (int64_t c0 = cs + 4 * lane; c0 < cend; c0 += 4 * kWave) {
+            const int r = (int)(c0 - cs);
+            const uint32_t a = lds_rd32(wq, r), b = lds_rd32(wq, r + 4);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t le = __builtin_amdgcn_alignbyte(b, a, (uint32_t)k);
+                try_cand(c0 + k, __builtin_bswap32(le));
+            }
+        }
+    } else {
+        for (int64_t c = cs + lane; c < cend; c += kWave)
+            if (c + 4 <= Cb) try_cand(c, be32_global(in + c));
     }
     for (int o = 32; o >= 1; o >>= 1) {
         lo = min(lo, (int64_t)__shfl_xor(lo, o));
@@ -165,7 +175,7 @@ struct Win {
     uint32_t v;
 };
 
-__device__ __forceinline__ void win_at(Win& w, const uint8_t* C, int clen, int pos, int lane) {
+__device__ __forceinline__ void win_at(Win& w, const lds8* C, int clen, int pos, int lane) {
     if (pos < w.base || pos >= w.base + kWave) {
         w.base = pos;
         const int p = pos + lane;
@@ -173,14 +183,14 @@ __device__ __forceinline__ void win_at(Win& w, const uint8_t* C, int clen, int p
     }
 }
 
-__device__ __forceinline__ int win_byte(Win& w, const uint8_t* C, int clen, int pos, int lane) {
+__device__ __forceinline__ int win_byte(Win& w, const lds8* C, int clen, int pos, int lane) {
     win_at(w, C, clen, pos, lane);
     return __builtin_amdgcn_readlane((int)w.v, pos - w.base);
 }
 
 // LZ4 length continuation starting at pos: adds bytes while they are 255,
 // the first non-255 byte ends it.  Returns -1 if it runs past clen.
-__device__ __forceinline__ int win_len(Win& w, const uint8_t* C, int clen, int& pos, int lane) {
+__device__ __forceinline__ int win_len(Win& w, const lds8* C, int clen, int& pos, int lane) {
     int add = 0;
     for (;;) {
         if (pos >= clen) return -1;
@@ -203,7 +213,8 @@ __device__ __forceinline__ int win_len(Win& w, const uint8_t* C, int clen, int& 
 
 // Decode C[0..clen) into D[0..n).  Returns 0, or an LZ4-style error
 // -(position)-1, or -91 - the only codes bshuf_decompress_lz4_block maps.
-__device__ int lz4_decode_block(const uint8_t* C, const int clen, uint8_t* D, const int n,
+template <int ABL = 0>
+__device__ int lz4_decode_block(const lds8* C, const int clen, lds8* D, const int n,
                                 const int lane) {
     int ip = 0, op = 0;
     Win w{-1000000, 0};
@@ -218,7 +229,8 @@ __device__ int lz4_decode_block(const uint8_t* C, const int clen, uint8_t* D, co
             lit += add;
         }
         if (q + lit > clen || op + lit > n) return -q - 1;
-        for (int i = lane; i < lit; i += kWave) D[op + i] = C[q + i];
+        if (!(ABL & 16))
+            for (int i = lane; i < lit; i += kWave) D[op + i] = C[q + i];
         op += lit;
         q += lit;
         if (q == clen) break;  // last sequence carries literals only
@@ -234,7 +246,8 @@ __device__ int lz4_decode_block(const uint8_t* C, const int clen, uint8_t* D, co
         }
         ml += kMinMatch;
         if (op + ml > n) return -q - 1;
-        if (off >= kWave || off >= ml) {
+        if (ABL & 32) {
+        } else if (off >= kWave || off >= ml) {
             // sources of chunk c were all written before chunk c starts
             for (int i = lane; i < ml; i += kWave) D[op + i] = D[op - off + i];
         } else {
@@ -253,6 +266,171 @@ __device__ int lz4_decode_block(const uint8_t* C, const int clen, uint8_t* D, co
     return op == n ? 0 : -91;
 }
 
+// ---------------------------------------------------------------------------
+// Decoder v2: 256-byte token window (lane l holds C[base+4l .. base+4l+3]; a
+// byte is one v_readlane + shift), dword-granular LDS copies, a fill path for
+// offset-1 matches (byte runs: the commonest match in bit planes) and whole
+// 256-byte chunks for offsets >= 256 (plane-stride matches).
+// ---------------------------------------------------------------------------
+struct Win4 {
+    int base;
+    uint32_t v;
+};
+
+__device__ __forceinline__ void w4_load(Win4& w, const lds8* C, int ccap, int pos, int lane) {
+    w.base = pos;
+    w.v = lds_rd32(C, min(pos + 4 * lane, ccap));
+}
+
+__device__ __forceinline__ uint32_t w4_byte(const Win4& w, int pos) {
+    const int t = pos - w.base;
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)w.v, t >> 2);
+    return (d >> ((t & 3) * 8)) & 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t w4_get(Win4& w, const lds8* C, int ccap, int pos, int lane) {
+    if (pos < w.base || pos >= w.base + 4 * kWave) w4_load(w, C, ccap, pos, lane);
+    return w4_byte(w, pos);
+}
+
+// LZ4 length continuation at q (bytes added while they are 255); -1 on overrun.
+__device__ __forceinline__ int w4_len(Win4& w, const lds8* C, int clen, int ccap, int& q,
+                                      int lane) {
+    int add = 0;
+    for (;;) {
+        if (q >= clen) return -1;
+        const uint32_t b = w4_get(w, C, ccap, q, lane);
+        q++;
+        add += (int)b;
+        if (b != 255u) return add;
+    }
+}
+
+// Write dwords covering D[op, op+len) with per-lane values from `gen(db)`
+// (db = first byte of the dword); the head dword keeps the bytes below op.
+// Bytes past op+len in the last dword are scratch: they are overwritten by the
+// next sequence before anything reads them (sources are always < op).
+template <class Gen>
+__device__ __forceinline__ void put_dwords(lds8* D, int op, int len, int lane, Gen gen) {
+    const int d0 = op >> 2, d1 = (op + len + 3) >> 2;
+    lds32* D32 = (lds32*)D;
+    for (int d = d0 + lane; d < d1; d += kWave) {
+        const int db = 4 * d;
+        uint32_t v = gen(db);
+        if (db < op) {
+            const uint32_t keep = (1u << (8 * (op - db))) - 1u;
+            v = (D32[d] & keep) | (v & ~keep);
+        }
+        D32[d] = v;
+    }
+}
+
+__device__ __forceinline__ uint32_t rd32_lo(const lds8* B, int p) {
+    // read32 at p where p may be up to 3 below 0: missing bytes are zero
+    const int pc = max(p, 0);
+    return lds_rd32(B, pc) << (8 * (pc - p));
+}
+
+__device__ __forceinline__ void copy_match(lds8* D, int op, int off, int ml, int lane) {
+    if (off == 1) {
+        const uint32_t fill = (uint32_t)D[op - 1] * 0x01010101u;
+        put_dwords(D, op, ml, lane, [&](int) { return fill; });
+        return;
+    }
+    if (off >= ml) {  // all sources are below op
+        put_dwords(D, op, ml, lane, [&](int db) { return rd32_lo(D, db - off); });
+        return;
+    }
+    if (off >= 4 * kWave) {  // 256-byte chunks: each chunk's sources precede it
+        for (int c = 0; c < ml; c += 4 * kWave) {
+            const int o = op + c;
+            put_dwords(D, o, min(4 * kWave, ml - c), lane,
+                       [&](int db) { return rd32_lo(D, db - off); });
+        }
+        return;
+    }
+    // short period: D[op+i] = D[op-off + i%off], all sources pre-existing
+    int r = (int)((float)lane * __builtin_amdgcn_rcpf((float)off) + 0.5f / (float)off);
+    r = lane - r * off;
+    if (r >= off) r -= off;
+    if (r < 0) r += off;
+    const int step = kWave % off;
+    for (int i = lane; i < ml; i += kWave) {
+        D[op + i] = D[op - off + r];
+        r += step;
+        if (r >= off) r -= off;
+    }
+}
+
+__device__ int lz4_decode_block_v2(const lds8* C, const int clen, const int ccap, lds8* D,
+                                   const int n, const int lane) {
+    int ip = 0, op = 0;
+    Win4 w;
+    w4_load(w, C, ccap, 0, lane);
+    for (;;) {
+        if (ip >= clen) return -ip - 1;
+        const uint32_t tok = w4_get(w, C, ccap, ip, lane);
+        int q = ip + 1;
+        int lit = (int)(tok >> 4);
+        if (lit == 15) {
+            const int add = w4_len(w, C, clen, ccap, q, lane);
+            if (add < 0) return -q - 1;
+            lit += add;
+        }
+        if (q + lit > clen || op + lit > n) return -q - 1;
+        if (lit) {
+            const int src = q - op;
+            put_dwords(D, op, lit, lane, [&](int db) { return rd32_lo(C, db + src); });
+        }
+        op += lit;
+        q += lit;
+        if (q == clen) break;  // last sequence carries literals only
+        if (q + 2 > clen) return -q - 1;
+        const int off = (int)(w4_get(w, C, ccap, q, lane) | (w4_get(w, C, ccap, q + 1, lane) << 8));
+        q += 2;
+        if (off == 0 || off > op) return -q - 1;
+        int ml = (int)(tok & 15u);
+        if (ml == 15) {
+            const int add = w4_len(w, C, clen, ccap, q, lane);
+            if (add < 0) return -q - 1;
+            ml += add;
+        }
+        ml += kMinMatch;
+        if (op + ml > n) return -q - 1;
+        copy_match(D, op, off, ml, lane);
+        op += ml;
+        ip = q;
+    }
+    return op == n ? 0 : -91;
+}
+
+// Inverse transpose D (LDS) -> dst (HBM), 4 groups per lane: one dword of
+// every plane per lane instead of single bytes.  Needs P % 4 == 0.
+template <int EK>
+__device__ __forceinline__ void untranspose_x4(const lds8* D, uint8_t* dst, int P, int lane) {
+    const lds32* D32 = (const lds32*)D;
+    const int P4 = P >> 2;
+    for (int q = lane; q < P4; q += kWave) {
+        uint32_t pl[8 * EK];
+#pragma unroll
+        for (int r = 0; r < 8 * EK; r++) pl[r] = D32[r * P4 + q];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t w[2 * EK];
+#pragma unroll
+            for (int i = 0; i < 2 * EK; i++) w[i] = 0;
+#pragma unroll
+            for (int b = 0; b < EK; b++) {
+                uint64_t v = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) v |= (uint64_t)((pl[8 * b + j] >> (8 * k)) & 0xFFu) << (8 * j);
+                scatter_byte_plane<EK>(w, b, tr8x8(v));
+            }
+            store_group<EK>(dst + (int64_t)(4 * q + k) * 8 * EK, w);
+        }
+    }
+}
+
 struct DecArgs {
     const uint8_t* in;
     int64_t in_nbytes;
@@ -263,6 +441,7 @@ struct DecArgs {
     Layout L;
     uint32_t maxlen;
     int32_t cap;     // LDS bytes reserved for the decoded block
+    int32_t ccap;    // readable LDS bytes of the record buffer
 };
 
 // Byte range [o0, o1) of block k's record ([BE32 c][c bytes]) in the stream.
@@ -285,14 +464,14 @@ __device__ __forceinline__ Span span_of(const DecArgs& a, int64_t k, int64_t nb)
 constexpr int kPayIters = 9;
 
 struct PayRegs {
-    uint4 v[kPayIters];
+    u32x4 v[kPayIters];
 };
 
 // Record bytes [o0, o1) are read as whole 16-byte granules aligned on the
 // absolute address (a granule never crosses a page: the extra bytes at either
 // end cannot fault and are never used); they land in LDS at Cbuf + (addr & 15).
-__device__ __forceinline__ const uint4* span_base(const DecArgs& a, const Span& sp) {
-    return reinterpret_cast<const uint4*>((uintptr_t)(a.in + sp.o0) & ~(uintptr_t)15);
+__device__ __forceinline__ const gbl128c* span_base(const DecArgs& a, const Span& sp) {
+    return g128_aligned_down(a.in + sp.o0);
 }
 __device__ __forceinline__ int span_shift(const DecArgs& a, const Span& sp) {
     return (int)((uintptr_t)(a.in + sp.o0) & 15);
@@ -306,7 +485,7 @@ __device__ __forceinline__ bool span_fits(const DecArgs& a, const Span& sp) {
 }
 
 __device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Span& sp, int lane) {
-    const uint4* g4 = span_base(a, sp);
+    const gbl128c* g4 = span_base(a, sp);
     const int nch = span_chunks(a, sp);
 #pragma unroll
     for (int it = 0; it < kPayIters; it++) {
@@ -316,25 +495,25 @@ __device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Sp
 }
 
 __device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, const Span& sp,
-                                         uint8_t* C, int lane) {
+                                         lds8* C, int lane) {
     const int nch = span_chunks(a, sp);
 #pragma unroll
     for (int it = 0; it < kPayIters; it++) {
         const int c = it * kWave + lane;
-        if (c < nch) reinterpret_cast<uint4*>(C)[c] = R.v[it];
+        if (c < nch) ((lds128*)C)[c] = R.v[it];
     }
 }
 
 // Persistent: workgroup w decodes blocks w, w+G, ...  Offsets are fetched two
 // blocks ahead and the next record's bytes one block ahead, into registers,
 // so HBM latency overlaps the LDS-bound LZ4 parse of the current block.
-template <int EK>
+template <int EK, int VAR>
 __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
     const int E = EK ? EK : a.L.E;
-    uint8_t* D = smem;                     // decoded (bit-shuffled) block
-    uint8_t* Cbuf = smem + a.cap + 16;     // record bytes, 16-aligned base
+    lds8* D = to_lds(smem);             // decoded (bit-shuffled) block
+    lds8* Cbuf = to_lds(smem) + a.cap + 16;  // record bytes, 16-aligned base
     const int64_t stride = gridDim.x;
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
@@ -354,9 +533,9 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         if (cur_in_regs) {
             land_pay(R, a, cur, Cbuf, lane);
         } else {
-            const uint4* g4 = span_base(a, cur);
+            const gbl128c* g4 = span_base(a, cur);
             const int nch = span_chunks(a, cur);
-            for (int c = lane; c < nch; c += kWave) reinterpret_cast<uint4*>(Cbuf)[c] = g4[c];
+            for (int c = lane; c < nch; c += kWave) ((lds128*)Cbuf)[c] = g4[c];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -367,27 +546,32 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         Span nxt2 = {0, 0};
         if (next + stride < nb) nxt2 = span_of(a, next + stride, nb);
 
-        const uint8_t* C = Cbuf + span_shift(a, cur);
+        const lds8* C = Cbuf + span_shift(a, cur);
         const int avail = (int)(cur.o1 - cur.o0);
         int status = 0, clen = 0;
         if (avail < 4) {
             status = -1000 - 1;
         } else {
-            clen = (int)be32_load(C);
+            clen = (int)(((uint32_t)C[0] << 24) | ((uint32_t)C[1] << 16) | ((uint32_t)C[2] << 8) | C[3]);
             const bool last = blk + 1 == nb;
             if (clen <= 0 || (uint32_t)clen > a.maxlen || clen + 4 > avail ||
                 (!last && clen + 4 != avail))
                 status = (clen + 4 > avail) ? -1000 - 1 : -91;
         }
         if (status == 0) {
-            const int r = lz4_decode_block(C + 4, clen, D, n, lane);
+            const int r = (VAR & 64) ? 0
+                          : (VAR & 2) ? lz4_decode_block_v2(C + 4, clen, a.ccap - 4, D, n, lane)
+                                      : lz4_decode_block<VAR>(C + 4, clen, D, n, lane);
             status = (r == -91) ? -91 : (r < 0 ? r - 1000 : 0);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (status == 0) {
+        if (status == 0 && !(VAR & 8)) {
             uint8_t* dst = a.out + blk * (int64_t)a.L.bs * E;
             if constexpr (EK != 0) {
+              if ((VAR & 4) && (P & 3) == 0) {
+                untranspose_x4<EK>(D, dst, P, lane);
+              } else {
                 for (int g = lane; g < P; g += kWave) {
                     uint32_t w[2 * EK];
 #pragma unroll
@@ -401,6 +585,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                     }
                     store_group<EK>(dst + (int64_t)g * 8 * EK, w);
                 }
+              }
             } else {
                 for (int i = lane; i < P * E; i += kWave) {
                     const int g = i / E, b = i - g * E;
@@ -513,18 +698,35 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15)};
+                  (int32_t)((nmax + 15) & ~15), 0};
         // decoded block + record (header, payload, 16-byte alignment slack)
-        const size_t lds = (size_t)a.cap + 16 + (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
+        const size_t rec = (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
+        const size_t lds = (size_t)a.cap + 16 + rec;
+        a.ccap = (int32_t)(rec - 16 - 8);  // record reads stay inside the buffer
         const bool aligned = ((uintptr_t)out & 15) == 0;
         const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
+        // tuning_variant(): bit1 the 256-byte-window block decoder (v2), bit2
+        // the 4-groups-per-lane inverse transpose -- both measured slower than
+        // the defaults on MI355X and kept for A/B; bits 3-6 are ABLATIONS for
+        // timing only (wrong output): 8 no output stores, 16 no literal copy,
+        // 32 no match copy, 64 no LZ4.
+        const int var = tuning_variant();
         const void* fn = nullptr;
         switch (ek) {
-            case 1: fn = reinterpret_cast<const void*>(k_lz4_decode<1>); break;
-            case 2: fn = reinterpret_cast<const void*>(k_lz4_decode<2>); break;
-            case 4: fn = reinterpret_cast<const void*>(k_lz4_decode<4>); break;
-            case 8: fn = reinterpret_cast<const void*>(k_lz4_decode<8>); break;
-            default: fn = reinterpret_cast<const void*>(k_lz4_decode<0>); break;
+            case 1: fn = reinterpret_cast<const void*>(k_lz4_decode<1, 0>); break;
+            case 2:
+                switch (var) {
+#define BSHUF_DEC_VAR(v) case v: fn = reinterpret_cast<const void*>(k_lz4_decode<2, v>); break;
+                    BSHUF_DEC_VAR(2) BSHUF_DEC_VAR(4) BSHUF_DEC_VAR(6) BSHUF_DEC_VAR(8)
+                    BSHUF_DEC_VAR(16) BSHUF_DEC_VAR(32) BSHUF_DEC_VAR(48) BSHUF_DEC_VAR(64)
+                    BSHUF_DEC_VAR(72)
+#undef BSHUF_DEC_VAR
+                    default: fn = reinterpret_cast<const void*>(k_lz4_decode<2, 0>); break;
+                }
+                break;
+            case 4: fn = reinterpret_cast<const void*>(k_lz4_decode<4, 0>); break;
+            case 8: fn = reinterpret_cast<const void*>(k_lz4_decode<8, 0>); break;
+            default: fn = reinterpret_cast<const void*>(k_lz4_decode<0, 0>); break;
         }
         if (lds > 65536) {
             e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -532,13 +734,9 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
         }
         const dim3 grid((unsigned)persistent_grid(fn, kWave, lds, nb));
         ProfScope prof("k_lz4_decode", s);
-        switch (ek) {
-            case 1: hipLaunchKernelGGL(k_lz4_decode<1>, grid, dim3(kWave), lds, s, a, nb); break;
-            case 2: hipLaunchKernelGGL(k_lz4_decode<2>, grid, dim3(kWave), lds, s, a, nb); break;
-            case 4: hipLaunchKernelGGL(k_lz4_decode<4>, grid, dim3(kWave), lds, s, a, nb); break;
-            case 8: hipLaunchKernelGGL(k_lz4_decode<8>, grid, dim3(kWave), lds, s, a, nb); break;
-            default: hipLaunchKernelGGL(k_lz4_decode<0>, grid, dim3(kWave), lds, s, a, nb); break;
-        }
+        void* args[] = {&a, const_cast<int64_t*>(&nb)};
+        e = hipLaunchKernel(fn, grid, dim3(kWave), args, lds, s);
+        if (e != hipSuccess) return e;
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -26,6 +26,8 @@
 // final, packed position.
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
+
 #include "launch.h"
 
 namespace bshuf {
@@ -78,6 +80,24 @@ struct EncArgs {
 // volatile generic pointer compiles to flat_load/flat_store sc0 sc1, whose
 // vmcnt(0) waits would drain every outstanding global load and store.
 // volatile keeps the tentative insert -> read-back order of the search.
+// Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
+// asm waits for its own result, so the compiler never reads it early.
+__device__ __forceinline__ uint32_t lds_addr(void* p) {
+    return (uint32_t)(uintptr_t)(lds8*)p;
+}
+__device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t addr, uint32_t mask, uint32_t data) {
+    uint32_t r;
+    asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(r) : "v"(addr), "v"(mask), "v"(data) : "memory");
+    return r;
+}
+__device__ __forceinline__ uint32_t lds_xchg_rtn(uint32_t addr, uint32_t data) {
+    uint32_t r;
+    asm volatile("ds_wrxchg_rtn_b32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(r) : "v"(addr), "v"(data) : "memory");
+    return r;
+}
+
 typedef __attribute__((address_space(3))) volatile uint16_t lds_vu16;
 typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 
@@ -96,10 +116,24 @@ struct Table {
         else
             ((lds_vu16*)base)[h] = (uint16_t)v;
     }
+    // Stores v at entry h and returns the entry as this lane found it.  The
+    // LDS unit serialises same-address lanes of one returning atomic in lane
+    // order (checked on the device before first use: lds_atomics_lane_ordered),
+    // so lane j gets the value of the highest LOWER active lane with the same
+    // entry, else the table's -- exactly the sequential insert-then-lookup.
+    __device__ __forceinline__ uint32_t exchange(uint32_t h, uint32_t v) const {
+        if constexpr (WIDE) {
+            return lds_xchg_rtn(lds_addr(base + 4 * h), v);
+        } else {
+            const uint32_t sh = 16u * (h & 1u);
+            const uint32_t old = lds_mskor_rtn(lds_addr(base + 4 * (h >> 1)), 0xFFFFu << sh, v << sh);
+            return (old >> sh) & 0xFFFFu;
+        }
+    }
 };
 
 template <bool WIDE>
-__device__ __forceinline__ uint32_t hash_at(const uint8_t* D, int p) {
+__device__ __forceinline__ uint32_t hash_at(const lds8* D, int p) {
     if constexpr (WIDE)
         return hash5(lds_rd64(D, p));
     else
@@ -169,7 +203,7 @@ __device__ __forceinline__ void ow_len(OutWin& W, uint32_t* out32, int& op, int 
 }
 
 // Copy D[from, from+len) (LDS) to the output stream at op.
-__device__ __forceinline__ void ow_copy(OutWin& W, uint32_t* out32, int& op, const uint8_t* D,
+__device__ __forceinline__ void ow_copy(OutWin& W, uint32_t* out32, int& op, const lds8* D,
                                         int from, int len, int lane) {
     while (len > 0) {
         if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
@@ -194,12 +228,20 @@ struct EmitWin {
     int lane;
     __device__ __forceinline__ void byte(int& op, uint32_t b) { ow_byte(W, out32, op, b, lane); }
     __device__ __forceinline__ void len(int& op, int v) { ow_len(W, out32, op, v, lane); }
-    __device__ __forceinline__ void copy(int& op, const uint8_t* D, int from, int n) {
+    __device__ __forceinline__ void copy(int& op, const lds8* D, int from, int n) {
         ow_copy(W, out32, op, D, from, n, lane);
     }
     __device__ __forceinline__ void finish(int op) {
         if (op > W.base) ow_flush(W, out32, lane);
     }
+};
+
+// Ablation only (timing): emits nothing, same parse.
+struct EmitNone {
+    __device__ __forceinline__ void byte(int& op, uint32_t) { op++; }
+    __device__ __forceinline__ void len(int& op, int v) { op += v / 255 + 1; }
+    __device__ __forceinline__ void copy(int& op, const lds8*, int, int n) { op += n; }
+    __device__ __forceinline__ void finish(int) {}
 };
 
 struct EmitBytes {
@@ -215,7 +257,7 @@ struct EmitBytes {
         for (int i = lane; i < nb; i += kWave) out[op + i] = (i < nb - 1) ? (uint8_t)255 : last;
         op += nb;
     }
-    __device__ __forceinline__ void copy(int& op, const uint8_t* D, int from, int n) {
+    __device__ __forceinline__ void copy(int& op, const lds8* D, int from, int n) {
         for (int i = lane; i < n; i += kWave) out[op + i] = D[from + i];
         op += n;
     }
@@ -234,7 +276,7 @@ struct CountOut {
     uint32_t tail;
 };
 
-__device__ __forceinline__ CountOut catch_and_count(const uint8_t* D, int n, int ip, int ref,
+__device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip, int ref,
                                                     int anchor, int mlimit, int lane) {
     CountOut r;
     // first forward window and backward bytes together
@@ -294,8 +336,8 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
 // out32 (4-byte aligned, room for the bound rounded up to 256).  Returns the
 // compressed size.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1,
 // notLimited output.
-template <bool WIDE, class Emit>
-__device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE> T, Emit& em,
+template <bool WIDE, bool READBACK, class Emit>
+__device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T, Emit& em,
                                 const int lane) {
     DIAG_DECL
     int op = 0, anchor = 0;
@@ -322,68 +364,100 @@ __device__ int lz4_encode_block(const uint8_t* D, const int n, const Table<WIDE>
                     const int pos_n = p0 + probe_offset(k0 + kWave + lane);
                     const uint32_t seq_nxt = lds_rd32(D, min(pos_n, n));
                     const uint32_t seq = seq_cur;
-                    uint32_t h = 0, cold = 0;
-                    if (valid) {
-                        if constexpr (WIDE)
-                            h = hash5(lds_rd64(D, pos));
-                        else
-                            h = hash4(seq);
-                        cold = T.get(h);
-                    }
-                    if (valid) T.put(h, (uint32_t)pos);
-                    const uint32_t rb = valid ? T.get(h) : (uint32_t)pos;
-                    const uint32_t dcold = lds_rd32(D, (int)cold);
-                    const bool loser = valid && rb != (uint32_t)pos;
-                    uint32_t cand = cold;
-                    int pred = -1;
-                    bool grouped = false, first = true;
-                    int next_member = kWave;
-                    uint64_t lmask = ballot(loser);
-                    COUNT(2, lmask ? 1 : 0);
-                    while (lmask) {
-                        const int l = ffs64(lmask);
-                        const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, l);
-                        const bool in_g = valid && h == hl;
-                        const uint64_t g = ballot(in_g);
-                        if (in_g) {
-                            grouped = true;
-                            const uint64_t below = g & ((1ull << lane) - 1ull);
-                            if (below) {
-                                pred = fls64(below);
-                                cand = (uint32_t)(p0 + probe_offset(k0 + pred));
-                                first = false;
-                            }
-                            const uint64_t above = lane == 63 ? 0ull : (g & (~0ull << (lane + 1)));
-                            next_member = above ? ffs64(above) : kWave;
-                        }
-                        lmask &= ~g;
-                    }
-                    // candidate bytes: the table's position, or the in-window predecessor's
-                    const uint32_t dpred = (uint32_t)__shfl((int)seq, pred < 0 ? lane : pred);
-                    const uint32_t dcand = pred < 0 ? dcold : dpred;
-                    bool ok = false;
-                    if (valid) {
-                        const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
-                        ok = near && dcand == seq;
-                    }
-                    const uint64_t mm = ballot(ok);
-                    if (mm) {
-                        const int js = ffs64(mm);
+                    if constexpr (!READBACK) {
+                        // one lane-ordered exchange = every lane's sequential
+                        // insert-then-lookup; candidate bytes come from the
+                        // (immutable) block in LDS
+                        uint32_t h = 0, cand = 0;
                         if (valid) {
-                            if (!grouped) {
-                                if (lane > js) T.put(h, cold);
-                            } else if (lane <= js && next_member > js) {
-                                T.put(h, (uint32_t)pos);
-                            } else if (first && lane > js) {
-                                T.put(h, cold);
-                            }
+                            if constexpr (WIDE)
+                                h = hash5(lds_rd64(D, pos));
+                            else
+                                h = hash4(seq);
+                            cand = T.exchange(h, (uint32_t)pos);
                         }
-                        mpos = p0 + probe_offset(k0 + js);
-                        mref = __builtin_amdgcn_readlane((int)cand, js);
-                        break;
+                        const uint32_t dcand = lds_rd32(D, (int)cand);
+                        bool ok = false;
+                        if (valid) {
+                            const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
+                            ok = near && dcand == seq;
+                        }
+                        const uint64_t mm = ballot(ok);
+                        if (mm) {
+                            const int js = ffs64(mm);
+                            mpos = p0 + probe_offset(k0 + js);
+                            // positions after the match were never inserted: the
+                            // first later lane of each entry puts back what it found
+                            // (found <= mpos: no lane between wrote that entry)
+                            if (valid && lane > js && cand <= (uint32_t)mpos) T.put(h, cand);
+                            mref = __builtin_amdgcn_readlane((int)cand, js);
+                            break;
+                        }
+                    } else {
+                        uint32_t h = 0, cold = 0;
+                        if (valid) {
+                            if constexpr (WIDE)
+                                h = hash5(lds_rd64(D, pos));
+                            else
+                                h = hash4(seq);
+                            cold = T.get(h);
+                        }
+                        if (valid) T.put(h, (uint32_t)pos);
+                        const uint32_t rb = valid ? T.get(h) : (uint32_t)pos;
+                        const uint32_t dcold = lds_rd32(D, (int)cold);
+                        const bool loser = valid && rb != (uint32_t)pos;
+                        uint32_t cand = cold;
+                        int pred = -1;
+                        bool grouped = false, first = true;
+                        int next_member = kWave;
+                        uint64_t lmask = ballot(loser);
+                        COUNT(2, lmask ? 1 : 0);
+                        while (lmask) {
+                            const int l = ffs64(lmask);
+                            const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, l);
+                            const bool in_g = valid && h == hl;
+                            const uint64_t g = ballot(in_g);
+                            if (in_g) {
+                                grouped = true;
+                                const uint64_t below = g & ((1ull << lane) - 1ull);
+                                if (below) {
+                                    pred = fls64(below);
+                                    cand = (uint32_t)(p0 + probe_offset(k0 + pred));
+                                    first = false;
+                                }
+                                const uint64_t above = lane == 63 ? 0ull : (g & (~0ull << (lane + 1)));
+                                next_member = above ? ffs64(above) : kWave;
+                            }
+                            lmask &= ~g;
+                        }
+                        // candidate bytes: the table's position, or the in-window predecessor's
+                        const uint32_t dpred = (uint32_t)__shfl((int)seq, pred < 0 ? lane : pred);
+                        const uint32_t dcand = pred < 0 ? dcold : dpred;
+                        bool ok = false;
+                        if (valid) {
+                            const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
+                            ok = near && dcand == seq;
+                        }
+                        const uint64_t mm = ballot(ok);
+                        if (mm) {
+                            const int js = ffs64(mm);
+                            if (valid) {
+                                if (!grouped) {
+                                    if (lane > js) T.put(h, cold);
+                                } else if (lane <= js && next_member > js) {
+                                    T.put(h, (uint32_t)pos);
+                                } else if (first && lane > js) {
+                                    T.put(h, cold);
+                                }
+                            }
+                            mpos = p0 + probe_offset(k0 + js);
+                            mref = __builtin_amdgcn_readlane((int)cand, js);
+                            break;
+                        }
+                        if (vmask == ~0ull && grouped && next_member == kWave)
+                            T.put(h, (uint32_t)pos);
                     }
                     if (vmask != ~0ull) break;  // ran past mflimit: last literals
-                    if (grouped && next_member == kWave) T.put(h, (uint32_t)pos);
                     seq_cur = seq_nxt;
                 }
             }
@@ -482,7 +556,7 @@ __device__ __forceinline__ void issue_block_loads(BlockRegs<EK>& R, const uint8_
 }
 
 template <int EK>
-__device__ __forceinline__ void transpose_regs_to_lds(const BlockRegs<EK>& R, uint8_t* D, int P,
+__device__ __forceinline__ void transpose_regs_to_lds(const BlockRegs<EK>& R, lds8* D, int P,
                                                       int g0, int lane) {
 #pragma unroll
     for (int it = 0; it < BlockRegs<EK>::kIters; it++) {
@@ -498,6 +572,57 @@ __device__ __forceinline__ void transpose_regs_to_lds(const BlockRegs<EK>& R, ui
     }
 }
 
+// 4-groups-per-lane variant (P % 4 == 0): lane q owns groups 4q..4q+3, i.e.
+// 32*EK contiguous input bytes, and writes ONE dword per plane to LDS.
+template <int EK>
+struct BlockRegs4 {
+    static constexpr int kIters = (EK ? 8192 / (kWave * 32 * EK) : 1) > 0
+                                      ? (EK ? 8192 / (kWave * 32 * EK) : 1) : 1;
+    uint32_t w[kIters][4][2 * (EK ? EK : 1)];
+};
+
+template <int EK>
+__device__ __forceinline__ void issue_block_loads4(BlockRegs4<EK>& R, const uint8_t* src, int P,
+                                                   int lane) {
+    const int P4 = P >> 2;
+#pragma unroll
+    for (int it = 0; it < BlockRegs4<EK>::kIters; it++) {
+        const int q = it * kWave + lane;
+        if (q < P4) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) load_group<EK>(src + ((int64_t)q * 4 + k) * 8 * EK, R.w[it][k]);
+        }
+    }
+}
+
+template <int EK>
+__device__ __forceinline__ void transpose4_regs_to_lds(const BlockRegs4<EK>& R, lds8* D, int P,
+                                                       int lane) {
+    const int P4 = P >> 2;
+    lds32* D32 = (lds32*)D;
+#pragma unroll
+    for (int it = 0; it < BlockRegs4<EK>::kIters; it++) {
+        const int q = it * kWave + lane;
+        if (q < P4) {
+            uint32_t pl[8 * EK];
+#pragma unroll
+            for (int r = 0; r < 8 * EK; r++) pl[r] = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+#pragma unroll
+                for (int b = 0; b < EK; b++) {
+                    const uint64_t v = tr8x8(gather_byte_plane<EK>(R.w[it][k], b));
+#pragma unroll
+                    for (int j = 0; j < 8; j++)
+                        pl[8 * b + j] |= (uint32_t)((v >> (8 * j)) & 0xFFu) << (8 * k);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 8 * EK; r++) D32[r * P4 + q] = pl[r];
+        }
+    }
+}
+
 // Persistent: workgroup w handles blocks w, w+G, w+2G, ...  While block k is
 // parsed out of LDS, the 8 KiB of block k+G are already in flight into
 // registers, so HBM latency hides under the (LDS-latency-bound) parse.
@@ -508,7 +633,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
     const int E = EK ? EK : a.L.E;
-    uint8_t* D = smem + kTableBytes;
+    lds8* D = to_lds(smem) + kTableBytes;
     const int64_t stride = gridDim.x;
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
@@ -516,11 +641,23 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     auto blk_src = [&](int64_t k) { return a.in + k * (int64_t)a.L.bs * E; };
 
     BlockRegs<EK> R;
+    BlockRegs4<EK> R4;
+    constexpr bool kX4 = (VAR & 4) == 0;  // 4-groups-per-lane transpose (default)
+    // insert/readback search window: the fallback when the device's LDS
+    // atomics do not serialise in lane order
+    constexpr bool kReadback = (VAR & 128) != 0;
     constexpr int kRegGroups = BlockRegs<EK>::kIters * kWave;
+    constexpr int kRegGroups4 = BlockRegs4<EK>::kIters * kWave * 4;
     // a block fits the prefetch registers when its groups fit
     auto fits = [&](int m) { return EK != 0 && m / 8 <= kRegGroups; };
-    if constexpr (EK != 0)
-        if (fits(blk_m(blk))) issue_block_loads<EK>(R, blk_src(blk), blk_m(blk) / 8, lane);
+    auto fits4 = [&](int m) { return kX4 && EK != 0 && (m / 8) % 4 == 0 && m / 8 <= kRegGroups4; };
+    if constexpr (EK != 0) {
+        const int m0 = blk_m(blk);
+        if (fits4(m0))
+            issue_block_loads4<EK>(R4, blk_src(blk), m0 / 8, lane);
+        else if (fits(m0))
+            issue_block_loads<EK>(R, blk_src(blk), m0 / 8, lane);
+    }
 
     for (;;) {
         const int m = blk_m(blk);
@@ -529,11 +666,13 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         const uint8_t* src = blk_src(blk);
         // zero the hash table (LZ4_initStream) and the read pad behind the block
         for (int i = lane; i < kTableBytes / 16; i += kWave)
-            reinterpret_cast<uint4*>(smem)[i] = make_uint4(0, 0, 0, 0);
-        if (lane < kDataPad / 4) reinterpret_cast<uint32_t*>(D + ((n + 3) & ~3))[lane] = 0;
+            ((lds128*)to_lds(smem))[i] = u32x4{0u, 0u, 0u, 0u};
+        if (lane < kDataPad / 4) ((lds32*)(D + ((n + 3) & ~3)))[lane] = 0;
         // bit transpose into LDS (bshuf_trans_bit_elem)
         if constexpr (EK != 0) {
-            if (fits(m)) {
+            if (fits4(m)) {
+                transpose4_regs_to_lds<EK>(R4, D, P, lane);
+            } else if (fits(m)) {
                 transpose_regs_to_lds<EK>(R, D, P, 0, lane);
             } else {
                 for (int g0 = 0; g0 < P; g0 += kRegGroups) {
@@ -562,23 +701,34 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         __builtin_amdgcn_wave_barrier();
         // prefetch the next block while this one is parsed
         const int64_t next = blk + stride;
-        if constexpr (EK != 0)
-            if (next < nb && fits(blk_m(next)))
-                issue_block_loads<EK>(R, blk_src(next), blk_m(next) / 8, lane);
+        if constexpr (EK != 0) {
+            if (next < nb) {
+                const int mn = blk_m(next);
+                if (fits4(mn))
+                    issue_block_loads4<EK>(R4, blk_src(next), mn / 8, lane);
+                else if (fits(mn))
+                    issue_block_loads<EK>(R, blk_src(next), mn / 8, lane);
+            }
+        }
 
         uint8_t* out = a.scratch + blk * a.slot;
         const Table<WIDE> T{smem};
         int c;
-        if constexpr (VAR == 0) {
+        if constexpr ((VAR & 64) != 0) {
+            c = 0;  // ablation: transpose + table setup only
+        } else if constexpr ((VAR & 8) != 0) {
+            EmitNone em;
+            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
+        } else if constexpr ((VAR & 1) == 0) {
             // default: byte-granular stores measured 11% faster than the
             // register window (tools/ab.py, 2 GiB G1: 9.13 vs 10.29 ms)
             EmitBytes em{out + 4, lane};
-            c = lz4_encode_block<WIDE>(D, n, T, em, lane);
+            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
         } else {
             EmitWin em;
             em.out32 = reinterpret_cast<uint32_t*>(out + 4);
             em.lane = lane;
-            c = lz4_encode_block<WIDE>(D, n, T, em, lane);
+            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
         }
         if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
@@ -606,19 +756,18 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
     const uintptr_t q0 = dst0 >> 4, q1 = (dst0 + (uintptr_t)len + 15) >> 4;
     for (uintptr_t q = q0 + threadIdx.x; q < q1; q += 256) {
         const int64_t s = (int64_t)(q * 16 - dst0);  // record offset of the chunk's first byte
-        uint8_t* d = reinterpret_cast<uint8_t*>(q * 16);
+        gbl8* d = (gbl8*)(q * 16);
         if (s >= 0 && s + 16 <= len) {
             const int64_t w0 = s >> 2;
             const uint32_t sh = (uint32_t)(s & 3);
             uint32_t x[5];
 #pragma unroll
             for (int i = 0; i < 5; i++) x[i] = rec32[w0 + i];
-            uint4 v;
-            v.x = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
-            v.y = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
-            v.z = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
-            v.w = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
-            *reinterpret_cast<uint4*>(d) = v;
+            const u32x4 v = {__builtin_amdgcn_alignbyte(x[1], x[0], sh),
+                             __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                             __builtin_amdgcn_alignbyte(x[3], x[2], sh),
+                             __builtin_amdgcn_alignbyte(x[4], x[3], sh)};
+            *(gbl128*)d = v;
         } else {
             for (int i = 0; i < 16; i++) {
                 const int64_t r = s + i;
@@ -637,10 +786,90 @@ __global__ void k_encode_finish(const uint64_t* offs, int64_t nblocks, const uin
     if (threadIdx.x == 0) *result = (int64_t)end + tail;
 }
 
+// Device check of the property Table::exchange relies on: same-address lanes
+// of ONE returning LDS atomic (ds_mskor_rtn_b32, ds_wrxchg_rtn_b32) are
+// processed in lane order.  512 patterns of active lanes / entries / halves;
+// each lane compares its returned value with the lane-order prediction.
+__global__ __launch_bounds__(64) void k_lds_order_check(int* fails) {
+    __shared__ uint32_t S[16];
+    const int lane = threadIdx.x;
+    int bad = 0;
+    for (int p = 0; p < 512; p++) {
+        if (lane < 16) S[lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int kind = p & 3;
+        const uint32_t ndw = kind == 0 ? 1u : (kind == 1 ? 2u : (kind == 2 ? 4u : 16u));
+        const bool xchg = (p >> 2) & 1;
+        auto pick = [&](int q) {
+            uint32_t x = (uint32_t)(p * 64 + q + 1) * 0x9E3779B1u;
+            x ^= x >> 15;
+            x *= 0x85EBCA77u;
+            return x ^ (x >> 13);
+        };
+        const uint32_t x = pick(lane);
+        const bool active = kind == 0 || x % 3u != 0u;
+        const uint32_t dw = (x >> 4) % ndw, sh = 16u * ((x >> 9) & 1u);
+        if (active) {
+            const uint32_t ad = lds_addr(S + dw), val = (uint32_t)(lane + 1) << sh;
+            const uint32_t r = xchg ? lds_xchg_rtn(ad, val) : lds_mskor_rtn(ad, 0xFFFFu << sh, val);
+            uint32_t e = 0;
+            for (int q = 0; q < lane; q++) {
+                const uint32_t y = pick(q);
+                if (!(kind == 0 || y % 3u != 0u) || (y >> 4) % ndw != dw) continue;
+                const uint32_t shq = 16u * ((y >> 9) & 1u), vq = (uint32_t)(q + 1) << shq;
+                e = xchg ? vq : ((e & ~(0xFFFFu << shq)) | vq);
+            }
+            bad += r != e;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (bad) atomicAdd(fails, bad);
+}
+
+// Once per device (cached): does k_lds_order_check pass?  Inside a stream
+// capture the check cannot run, and the encoder takes the readback path.
+bool lds_atomics_lane_ordered(hipStream_t s) {
+    static std::atomic<int> state[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    const int st = state[dev].load(std::memory_order_acquire);
+    if (st) return st == 1;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return false;
+    int* d = nullptr;
+    int h = -1;
+    bool ok = hipMalloc(&d, sizeof(int)) == hipSuccess;
+    ok = ok && hipMemsetAsync(d, 0, sizeof(int), s) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_lds_order_check, dim3(1), dim3(kWave), 0, s, d);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+    }
+    if (d) (void)hipFree(d);
+    const bool ordered = ok && h == 0;
+    if (ok) state[dev].store(ordered ? 1 : 2, std::memory_order_release);
+    return ordered;
+}
+
 template <int EK, bool WIDE, int VAR = 0>
 hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s) {
-    if constexpr (EK == 2 && !WIDE && VAR == 0)
-        if (tuning_variant() == 1) return launch_enc_t<2, false, 1>(a, nb, lds, s);  // window
+    if constexpr (EK == 2 && !WIDE && VAR == 0) {
+        // A/B + ablations (tools/ab.py, tools/ablate.py): 1 register-window
+        // emitter; 8 no output stores; 64 no LZ4 parse (timing only)
+        const int v = tuning_variant();
+        if (v == 1) return launch_enc_t<2, false, 1>(a, nb, lds, s);
+        if (v == 8) return launch_enc_t<2, false, 8>(a, nb, lds, s);
+        if (v == 64) return launch_enc_t<2, false, 64>(a, nb, lds, s);
+        if (v == 4) return launch_enc_t<2, false, 4>(a, nb, lds, s);
+        if (v == 68) return launch_enc_t<2, false, 68>(a, nb, lds, s);
+        if (v == 128) return launch_enc_t<2, false, 128>(a, nb, lds, s);
+    }
+    if constexpr (VAR == 0) {  // (timing-only variants assume the property)
+        if (!lds_atomics_lane_ordered(s)) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
+    }
     auto fn = k_lz4_encode<EK, WIDE, VAR>;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),

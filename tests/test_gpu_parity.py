@@ -120,6 +120,30 @@ def test_lz4_matches_oracle(bs, oracle, kind):
                 assert back.tobytes() == arr.tobytes(), (kind, E, n, block)
 
 
+@pytest.mark.parametrize("variant", [128, 2, 4, 6])
+def test_alternate_kernel_paths_match_oracle(bs, oracle, variant):
+    """The selectable non-default paths (elem_size 2): 128 = encoder
+    insert/readback search window (the fallback when the LDS-atomic lane-order
+    self-check fails); 2 = 256-byte-window block decoder; 4 = 4-groups-per-lane
+    inverse transpose; 6 = both."""
+    rng = np.random.default_rng(variant)
+    cases = [oracle.gen_g1(3 * 4096 + 1005),
+             (rng.integers(-2, 3, 50000).cumsum() % 97).astype(np.int16),
+             np.repeat(rng.integers(0, 4, 9000), 7).astype(np.int16),
+             rng.integers(0, 1 << 16, 20000).astype(np.uint16)]
+    try:
+        bs.lib.bshuf_set_variant(variant)
+        for arr in cases:
+            for block in [0, 64, 2048]:
+                want = oracle.compress_lz4(arr, block)
+                got = bs.compress_lz4(arr, block)
+                assert got.tobytes() == want.tobytes(), (variant, arr.size, block)
+                back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
+                assert back.tobytes() == arr.tobytes(), (variant, arr.size, block)
+    finally:
+        bs.lib.bshuf_set_variant(0)
+
+
 def test_lz4_u32_table_path(bs, oracle):
     """Blocks of >= 65547 bytes switch LZ4 to the byU32 table + hash5
     (lz4/lz4.c:1389-1393, 785-795)."""
