@@ -87,13 +87,16 @@ size_t enc_ws(const Plan& p, EncodeBufs* b, uint8_t* base) {
     return c.off;
 }
 
-size_t dec_ws(const Plan& p, int64_t blocks_end, bool need_index, DecodeBufs* b, uint8_t* base) {
+size_t dec_ws(const Plan& p, int64_t blocks_end, int64_t in_nbytes, bool need_index, DecodeBufs* b,
+              uint8_t* base) {
     Carver c{base};
     DecodeBufs x;
     x.chunk = index_chunk_bytes(p.L);
     x.nchunks = blocks_end > 0 ? (blocks_end + x.chunk - 1) / x.chunk : 0;
     x.offs = c.take<uint64_t>((size_t)p.nb * 8 + 8);
     x.status = c.take<int64_t>((size_t)p.nb * 8 + 8);
+    // one u32 per 3 stream bytes (a sequence takes >= 3), + a 64-lane prefetch
+    x.seq = c.take<uint32_t>(((size_t)in_nbytes / 3 + 80) * 4);
     x.exits = c.take<int64_t>((size_t)x.nchunks * 8 + 8);
     x.cnt = c.take<uint64_t>((size_t)(x.nchunks + 1) * 8);
     x.base = c.take<uint64_t>((size_t)(x.nchunks + 1) * 8);
@@ -223,7 +226,7 @@ size_t bshuf_decompress_lz4_dev_workspace(size_t in_nbytes, size_t size, size_t 
     Plan p;
     if (make_plan(size, elem_size, block_size, p)) return 0;
     const int64_t cb = (int64_t)in_nbytes - p.tail;
-    return dec_ws(p, cb > 0 ? cb : 0, true, nullptr, nullptr);
+    return dec_ws(p, cb > 0 ? cb : 0, (int64_t)in_nbytes, true, nullptr, nullptr);
 }
 
 int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, size_t size,
@@ -239,7 +242,7 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
     int64_t cb = (int64_t)in_nbytes - p.tail;
     if (cb < 0) cb = 0;
     const bool need_index = block_offsets == nullptr;
-    const size_t need = dec_ws(p, cb, need_index, nullptr, nullptr);
+    const size_t need = dec_ws(p, cb, (int64_t)in_nbytes, need_index, nullptr, nullptr);
     DevBuf own;
     if (!ws) {
         if (own.alloc(need, s) != hipSuccess) return -1;
@@ -248,7 +251,7 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
         return kErrUnsupported;
     }
     DecodeBufs b;
-    dec_ws(p, cb, need_index, &b, (uint8_t*)ws);
+    dec_ws(p, cb, (int64_t)in_nbytes, need_index, &b, (uint8_t*)ws);
     const uint8_t* i8 = (const uint8_t*)in;
     if (need_index) {
         if (launch_index(i8, cb, p.L, b, s) != hipSuccess) return kErrHip;

@@ -56,6 +56,7 @@ int64_t max_device_block_bytes();
 struct DecodeBufs {
     uint64_t* offs;     // nblocks u64: header offset of each block
     int64_t* status;    // nblocks i64: consumed bytes or error code per block
+    uint32_t* seq;      // token positions of the two-phase decode
     // block index rebuild (unused when offsets are supplied)
     int64_t* exits;     // nchunks
     uint64_t* cnt;      // nchunks + 1

@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "launch.h"
+#include "lz4_scan.h"
 
 namespace bshuf {
 
@@ -169,264 +170,157 @@ __global__ void k_idx_check(const uint64_t* base, int64_t nchunks, int64_t nbloc
 // Per-block LZ4 decode
 // ---------------------------------------------------------------------------
 
-// 64-byte window over the compressed block in LDS: lane l holds C[base + l].
-struct Win {
-    int base;
-    uint32_t v;
-};
-
-__device__ __forceinline__ void win_at(Win& w, const lds8* C, int clen, int pos, int lane) {
-    if (pos < w.base || pos >= w.base + kWave) {
-        w.base = pos;
-        const int p = pos + lane;
-        w.v = p < clen ? C[p] : 0u;
-    }
-}
-
-__device__ __forceinline__ int win_byte(Win& w, const lds8* C, int clen, int pos, int lane) {
-    win_at(w, C, clen, pos, lane);
-    return __builtin_amdgcn_readlane((int)w.v, pos - w.base);
-}
-
-// LZ4 length continuation starting at pos: adds bytes while they are 255,
-// the first non-255 byte ends it.  Returns -1 if it runs past clen.
-__device__ __forceinline__ int win_len(Win& w, const lds8* C, int clen, int& pos, int lane) {
-    int add = 0;
-    for (;;) {
-        if (pos >= clen) return -1;
-        win_at(w, C, clen, pos, lane);
-        const int o = pos - w.base;
-        const bool in = lane >= o && w.base + lane < clen;
-        const uint64_t nm = ballot(in && w.v != 255u) | ballot(!(w.base + lane < clen) && lane >= o);
-        if (nm == 0) {
-            add += 255 * (kWave - o);
-            pos = w.base + kWave;
-            continue;
-        }
-        const int f = ffs64(nm);
-        if (w.base + f >= clen) return -1;
-        add += 255 * (f - o) + __builtin_amdgcn_readlane((int)w.v, f);
-        pos = w.base + f + 1;
-        return add;
-    }
-}
-
-// Decode C[0..clen) into D[0..n).  Returns 0, or an LZ4-style error
-// -(position)-1, or -91 - the only codes bshuf_decompress_lz4_block maps.
-template <int ABL = 0>
-__device__ int lz4_decode_block(const lds8* C, const int clen, lds8* D, const int n,
-                                const int lane) {
-    int ip = 0, op = 0;
-    Win w{-1000000, 0};
-    for (;;) {
-        if (ip >= clen) return -ip - 1;
-        const int tok = win_byte(w, C, clen, ip, lane);
-        int q = ip + 1;
-        int lit = tok >> 4;
-        if (lit == 15) {
-            const int add = win_len(w, C, clen, q, lane);
-            if (add < 0) return -q - 1;
-            lit += add;
-        }
-        if (q + lit > clen || op + lit > n) return -q - 1;
-        if (!(ABL & 16))
-            for (int i = lane; i < lit; i += kWave) D[op + i] = C[q + i];
-        op += lit;
-        q += lit;
-        if (q == clen) break;  // last sequence carries literals only
-        if (q + 2 > clen) return -q - 1;
-        const int off = win_byte(w, C, clen, q, lane) | (win_byte(w, C, clen, q + 1, lane) << 8);
-        q += 2;
-        if (off == 0 || off > op) return -q - 1;
-        int ml = tok & 15;
-        if (ml == 15) {
-            const int add = win_len(w, C, clen, q, lane);
-            if (add < 0) return -q - 1;
-            ml += add;
-        }
-        ml += kMinMatch;
-        if (op + ml > n) return -q - 1;
-        if (ABL & 32) {
-        } else if (off >= kWave || off >= ml) {
-            // sources of chunk c were all written before chunk c starts
-            for (int i = lane; i < ml; i += kWave) D[op + i] = D[op - off + i];
-        } else {
-            // short period: output is periodic with period off
-            int r = lane % off;
-            const int step = kWave % off;
-            for (int i = lane; i < ml; i += kWave) {
-                D[op + i] = D[op - off + r];
-                r += step;
-                if (r >= off) r -= off;
-            }
-        }
-        op += ml;
-        ip = q;
-    }
-    return op == n ? 0 : -91;
-}
-
 // ---------------------------------------------------------------------------
-// Decoder v2: 256-byte token window (lane l holds C[base+4l .. base+4l+3]; a
-// byte is one v_readlane + shift), dword-granular LDS copies, a fill path for
-// offset-1 matches (byte runs: the commonest match in bit planes) and whole
-// 256-byte chunks for offsets >= 256 (plane-stride matches).
+// Two-phase decode (default).  Phase 1 (k_seq_scan, one LANE per block) walks
+// each record's token chain straight from HBM, applies every check of
+// LZ4_decompress_safe with the same error positions, and stores the payload
+// position of each sequence's token.  Phase 2 (lz4_exec_block, one wave per
+// block) then has no serial walk left: 64 lanes decode 64 sequences at once,
+// a DPP prefix sum places them, every literal run is copied in parallel, and
+// the matches run in batches of consecutive sequences that cannot depend on
+// each other (their sources end before the batch's first output byte).
 // ---------------------------------------------------------------------------
-struct Win4 {
-    int base;
-    uint32_t v;
-};
 
-__device__ __forceinline__ void w4_load(Win4& w, const lds8* C, int ccap, int pos, int lane) {
-    w.base = pos;
-    w.v = lds_rd32(C, min(pos + 4 * lane, ccap));
+// One lane copies n <= 16 bytes; S and Dd are 4-aligned LDS bases.
+__device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int dp, int n) {
+    const lds32* w = (const lds32*)(S + (sp & ~3));
+    const uint32_t sh = (uint32_t)(sp & 3);
+    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+    const uint32_t v[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        if (i < n) Dd[dp + i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
 }
 
-__device__ __forceinline__ uint32_t w4_byte(const Win4& w, int pos) {
-    const int t = pos - w.base;
-    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)w.v, t >> 2);
-    return (d >> ((t & 3) * 8)) & 0xFFu;
-}
-
-__device__ __forceinline__ uint32_t w4_get(Win4& w, const lds8* C, int ccap, int pos, int lane) {
-    if (pos < w.base || pos >= w.base + 4 * kWave) w4_load(w, C, ccap, pos, lane);
-    return w4_byte(w, pos);
-}
-
-// LZ4 length continuation at q (bytes added while they are 255); -1 on overrun.
-__device__ __forceinline__ int w4_len(Win4& w, const lds8* C, int clen, int ccap, int& q,
-                                      int lane) {
-    int add = 0;
-    for (;;) {
-        if (q >= clen) return -1;
-        const uint32_t b = w4_get(w, C, ccap, q, lane);
-        q++;
-        add += (int)b;
-        if (b != 255u) return add;
+// The whole wave copies n bytes whose source ends at or before the
+// destination starts (or lies in another buffer).  Long runs go as aligned
+// destination dwords built from two source dwords, edges byte-wise.
+__device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int dp, int n, int lane) {
+    if (n <= kWave) {
+        if (lane < n) Dd[dp + lane] = S[sp + lane];
+        return;
+    }
+    const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
+    const int head = q0 - dp, tailn = dp + n - q1;
+    const int e = lane < 4 ? lane : n - tailn + (lane - 4);
+    if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn)) Dd[dp + e] = S[sp + e];
+    const int nw = (q1 - q0) >> 2;
+    for (int c = lane; c < nw; c += kWave) {
+        const int s2 = sp + head + 4 * c;
+        const lds32* w = (const lds32*)(S + (s2 & ~3));
+        ((lds32*)(Dd + q0))[c] = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(s2 & 3));
     }
 }
 
-// Write dwords covering D[op, op+len) with per-lane values from `gen(db)`
-// (db = first byte of the dword); the head dword keeps the bytes below op.
-// Bytes past op+len in the last dword are scratch: they are overwritten by the
-// next sequence before anything reads them (sources are always < op).
-template <class Gen>
-__device__ __forceinline__ void put_dwords(lds8* D, int op, int len, int lane, Gen gen) {
-    const int d0 = op >> 2, d1 = (op + len + 3) >> 2;
-    lds32* D32 = (lds32*)D;
-    for (int d = d0 + lane; d < d1; d += kWave) {
-        const int db = 4 * d;
-        uint32_t v = gen(db);
-        if (db < op) {
-            const uint32_t keep = (1u << (8 * (op - db))) - 1u;
-            v = (D32[d] & keep) | (v & ~keep);
+// The whole wave runs a match that overlaps its own output (off < ml): the
+// output is periodic with period off.  Offset 0 (accepted by
+// LZ4_decompress_safe, never emitted by a compressor) writes zeros, as LZ4's
+// LZ4_write32(op, 0) seed makes it (lz4/lz4.c:501, 2407).
+__device__ __forceinline__ void wave_fill(lds8* D, int op, int off, int ml, int lane) {
+    const int s = op - off;
+    if (off == 0) {
+        for (int i = lane; i < ml; i += kWave) D[op + i] = 0;
+    } else if (off >= kWave) {
+        // every 64-byte chunk reads bytes written by earlier chunks
+        for (int i = lane; i < ml; i += kWave) D[op + i] = D[s + i];
+    } else {
+        int r = lane % off;
+        const int step = kWave % off;
+        for (int i = lane; i < ml; i += kWave) {
+            D[op + i] = D[s + r];
+            r += step;
+            if (r >= off) r -= off;
         }
-        D32[d] = v;
     }
 }
 
-__device__ __forceinline__ uint32_t rd32_lo(const lds8* B, int p) {
-    // read32 at p where p may be up to 3 below 0: missing bytes are zero
-    const int pc = max(p, 0);
-    return lds_rd32(B, pc) << (8 * (pc - p));
+// Inclusive prefix sum over the 64 lanes (Hillis-Steele over __shfl_up).
+__device__ __forceinline__ int wave_incl_sum(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
 }
 
-__device__ __forceinline__ void copy_match(lds8* D, int op, int off, int ml, int lane) {
-    if (off == 1) {
-        const uint32_t fill = (uint32_t)D[op - 1] * 0x01010101u;
-        put_dwords(D, op, ml, lane, [&](int) { return fill; });
-        return;
-    }
-    if (off >= ml) {  // all sources are below op
-        put_dwords(D, op, ml, lane, [&](int db) { return rd32_lo(D, db - off); });
-        return;
-    }
-    if (off >= 4 * kWave) {  // 256-byte chunks: each chunk's sources precede it
-        for (int c = 0; c < ml; c += 4 * kWave) {
-            const int o = op + c;
-            put_dwords(D, o, min(4 * kWave, ml - c), lane,
-                       [&](int db) { return rd32_lo(D, db - off); });
-        }
-        return;
-    }
-    // short period: D[op+i] = D[op-off + i%off], all sources pre-existing
-    int r = (int)((float)lane * __builtin_amdgcn_rcpf((float)off) + 0.5f / (float)off);
-    r = lane - r * off;
-    if (r >= off) r -= off;
-    if (r < 0) r += off;
-    const int step = kWave % off;
-    for (int i = lane; i < ml; i += kWave) {
-        D[op + i] = D[op - off + r];
-        r += step;
-        if (r >= off) r -= off;
-    }
-}
-
-__device__ int lz4_decode_block_v2(const lds8* C, const int clen, const int ccap, lds8* D,
-                                   const int n, const int lane) {
-    int ip = 0, op = 0;
-    Win4 w;
-    w4_load(w, C, ccap, 0, lane);
-    for (;;) {
-        if (ip >= clen) return -ip - 1;
-        const uint32_t tok = w4_get(w, C, ccap, ip, lane);
-        int q = ip + 1;
-        int lit = (int)(tok >> 4);
+// Phase 2 for one block.  The record payload starts at byte cp of the
+// 4-aligned LDS buffer Cb; pos[0..nseq) are its token positions (payload-
+// relative, validated by the scan); pos0 is this lane's prefetched pos[lane].
+__device__ void lz4_exec_block(const lds8* Cb, const int cp, lds8* D,
+                               const uint32_t* __restrict__ pos, const int nseq, uint32_t pos0,
+                               const int lane) {
+    int opb = 0;
+    uint32_t pnext = pos0;
+    for (int c0 = 0; c0 < nseq; c0 += kWave) {
+        const int j = c0 + lane;
+        const bool act = j < nseq;
+        const int tp = act ? (int)pnext : 0;
+        if (c0 + kWave < nseq && c0 + kWave + lane < nseq) pnext = pos[c0 + kWave + lane];
+        // ---- sequence fields, lane = sequence
+        const int p = cp + tp;
+        const uint32_t x = lds_rd32(Cb, p);
+        const int tok = (int)(x & 255u);
+        int lit = act ? tok >> 4 : 0;
+        int q = p + 1;
         if (lit == 15) {
-            const int add = w4_len(w, C, clen, ccap, q, lane);
-            if (add < 0) return -q - 1;
-            lit += add;
+            int b;
+            do {
+                b = Cb[q++];
+                lit += b;
+            } while (b == 255);
         }
-        if (q + lit > clen || op + lit > n) return -q - 1;
-        if (lit) {
-            const int src = q - op;
-            put_dwords(D, op, lit, lane, [&](int db) { return rd32_lo(C, db + src); });
-        }
-        op += lit;
+        const int lsrc = q;
         q += lit;
-        if (q == clen) break;  // last sequence carries literals only
-        if (q + 2 > clen) return -q - 1;
-        const int off = (int)(w4_get(w, C, ccap, q, lane) | (w4_get(w, C, ccap, q + 1, lane) << 8));
-        q += 2;
-        if (off == 0 || off > op) return -q - 1;
-        int ml = (int)(tok & 15u);
-        if (ml == 15) {
-            const int add = w4_len(w, C, clen, ccap, q, lane);
-            if (add < 0) return -q - 1;
-            ml += add;
-        }
-        ml += kMinMatch;
-        if (op + ml > n) return -q - 1;
-        copy_match(D, op, off, ml, lane);
-        op += ml;
-        ip = q;
-    }
-    return op == n ? 0 : -91;
-}
-
-// Inverse transpose D (LDS) -> dst (HBM), 4 groups per lane: one dword of
-// every plane per lane instead of single bytes.  Needs P % 4 == 0.
-template <int EK>
-__device__ __forceinline__ void untranspose_x4(const lds8* D, uint8_t* dst, int P, int lane) {
-    const lds32* D32 = (const lds32*)D;
-    const int P4 = P >> 2;
-    for (int q = lane; q < P4; q += kWave) {
-        uint32_t pl[8 * EK];
-#pragma unroll
-        for (int r = 0; r < 8 * EK; r++) pl[r] = D32[r * P4 + q];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            uint32_t w[2 * EK];
-#pragma unroll
-            for (int i = 0; i < 2 * EK; i++) w[i] = 0;
-#pragma unroll
-            for (int b = 0; b < EK; b++) {
-                uint64_t v = 0;
-#pragma unroll
-                for (int j = 0; j < 8; j++) v |= (uint64_t)((pl[8 * b + j] >> (8 * k)) & 0xFFu) << (8 * j);
-                scatter_byte_plane<EK>(w, b, tr8x8(v));
+        int off = 0, ml = 0;
+        if (act && j + 1 < nseq) {  // the last sequence has no match
+            off = lit == 0 ? (int)((x >> 8) & 0xFFFFu) : (int)(lds_rd32(Cb, q) & 0xFFFFu);
+            q += 2;
+            ml = tok & 15;
+            if (ml == 15) {
+                int b;
+                do {
+                    b = Cb[q++];
+                    ml += b;
+                } while (b == 255);
             }
-            store_group<EK>(dst + (int64_t)(4 * q + k) * 8 * EK, w);
+            ml += kMinMatch;
+        }
+        const int len = lit + ml;
+        const int incl = wave_incl_sum(len, lane);
+        const int op = opb + incl - len;
+        opb += __builtin_amdgcn_readlane(incl, kWave - 1);
+        // ---- literals: short runs per lane, long runs by the whole wave
+        if (lit > 0 && lit <= 16) lane_copy16(Cb, lsrc, D, op, lit);
+        for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
+            const int l = ffs64(lm);
+            wave_copy(Cb, __builtin_amdgcn_readlane(lsrc, l), D, __builtin_amdgcn_readlane(op, l),
+                      __builtin_amdgcn_readlane(lit, l), lane);
+        }
+        // ---- matches, in batches of mutually independent sequences
+        const int mop = op + lit;
+        uint64_t todo = ballot(ml > 0);
+        while (todo) {
+            const int f = ffs64(todo);
+            const int opf = __builtin_amdgcn_readlane(mop, f);
+            const bool stop = lane > f && ml > 0 && (off < ml || mop - off + ml > opf);
+            const uint64_t sm = ballot(stop);
+            const int g = sm ? ffs64(sm) : kWave;
+            const bool inb = lane >= f && lane < g && ml > 0;
+            const bool coop = inb && (ml > 16 || off < ml);  // only the head can overlap itself
+            if (inb && !coop) lane_copy16(D, mop - off, D, mop, ml);
+            for (uint64_t cm = ballot(coop); cm; cm &= cm - 1) {
+                const int l = ffs64(cm);
+                const int lo = __builtin_amdgcn_readlane(off, l);
+                const int lm = __builtin_amdgcn_readlane(ml, l);
+                const int lp = __builtin_amdgcn_readlane(mop, l);
+                if (lo >= lm)
+                    wave_copy(D, lp - lo, D, lp, lm, lane);
+                else
+                    wave_fill(D, lp, lo, lm, lane);
+            }
+            todo &= g >= kWave ? 0ull : (~0ull << g);
         }
     }
 }
@@ -441,7 +335,7 @@ struct DecArgs {
     Layout L;
     uint32_t maxlen;
     int32_t cap;     // LDS bytes reserved for the decoded block
-    int32_t ccap;    // readable LDS bytes of the record buffer
+    uint32_t* seq;   // token positions (k_seq_scan -> lz4_exec_block)
 };
 
 // Byte range [o0, o1) of block k's record ([BE32 c][c bytes]) in the stream.
@@ -449,22 +343,15 @@ struct DecArgs {
 // the last record is bounded by its worst-case size.
 struct Span {
     int64_t o0, o1;
+    int64_t scan;  // k_seq_scan's result: sequence count, or the block's error code
 };
-
-__device__ __forceinline__ Span span_of(const DecArgs& a, int64_t k, int64_t nb) {
-    Span sp;
-    sp.o0 = (int64_t)a.offs[k];
-    sp.o1 = (k + 1 < nb) ? (int64_t)a.offs[k + 1] : sp.o0 + 4 + (int64_t)a.maxlen;
-    if (sp.o1 > a.in_nbytes) sp.o1 = a.in_nbytes;
-    if (sp.o0 > sp.o1) sp.o0 = sp.o1;
-    return sp;
-}
 
 // 16-byte chunks covering a record of an 8 KiB block: (8244 + 30) / 16 / 64 -> 9.
 constexpr int kPayIters = 9;
 
 struct PayRegs {
     u32x4 v[kPayIters];
+    uint32_t pos;  // token position of sequence `lane` (two-phase path)
 };
 
 // Record bytes [o0, o1) are read as whole 16-byte granules aligned on the
@@ -492,6 +379,7 @@ __device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Sp
         const int c = it * kWave + lane;
         if (c < nch) R.v[it] = g4[c];
     }
+    R.pos = a.seq[sp.o0 / 3 + lane];
 }
 
 __device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, const Span& sp,
@@ -504,9 +392,129 @@ __device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, con
     }
 }
 
-// Persistent: workgroup w decodes blocks w, w+G, ...  Offsets are fetched two
-// blocks ahead and the next record's bytes one block ahead, into registers,
-// so HBM latency overlaps the LDS-bound LZ4 parse of the current block.
+// Raw offsets of a record, loaded one block before they are turned into a
+// Span, so the load's latency is covered by a parse.  Lanes 0 and 1 load
+// offs[k] and offs[k+1]: a lane-varying value stays in VGPRs until
+// span_from's readlanes (a uniform load would be moved to SGPRs, and waited
+// for, right away).
+struct OffRegs {
+    uint64_t v;
+    bool last;  // k is the last block: the record end is bounded by maxlen
+};
+
+__device__ __forceinline__ OffRegs issue_offs(const DecArgs& a, int64_t k, int64_t nb, int lane) {
+    OffRegs r;
+    r.v = 0;
+    r.last = k + 1 >= nb;
+    if (lane < 2) {
+        if (k + lane < nb) r.v = a.offs[k + lane];
+    } else if (lane == 2) {
+        r.v = (uint64_t)a.status[k];  // the scan's verdict
+    }
+    return r;
+}
+
+__device__ __forceinline__ Span span_from(const DecArgs& a, const OffRegs& r) {
+    auto rl = [&](int l) {
+        return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(r.v >> 32), l) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)r.v, l));
+    };
+    Span sp;
+    sp.o0 = rl(0);
+    sp.o1 = r.last ? sp.o0 + 4 + (int64_t)a.maxlen : rl(1);
+    sp.scan = rl(2);
+    if (sp.o1 > a.in_nbytes) sp.o1 = a.in_nbytes;
+    if (sp.o0 > sp.o1) sp.o0 = sp.o1;
+    return sp;
+}
+
+// Phase 1: one lane per block.  A 32-byte window of the lane's record lives
+// in registers as two absolute-aligned granules (a granule never crosses a
+// page; the second is loaded only when it holds payload bytes).
+struct GWin {
+    int w0;  // payload position of window byte 0
+    u32x4 a, b;
+};
+
+__device__ __forceinline__ uint32_t gw_byte(GWin& g, const uint8_t* P, int clen, int p) {
+    if ((unsigned)(p - g.w0) >= 32u) {
+        const uint8_t* ap = P + p;
+        g.w0 = p - (int)((uintptr_t)ap & 15);
+        const gbl128c* q = g128_aligned_down(ap);
+        g.a = q[0];
+        if (g.w0 + 16 < clen) g.b = q[1];
+    }
+    const int t = p - g.w0;
+    const u32x4 v = t < 16 ? g.a : g.b;
+    const int d = (t >> 2) & 3;
+    const uint32_t x = d == 0 ? v.x : (d == 1 ? v.y : (d == 2 ? v.z : v.w));
+    return (x >> (8 * (t & 3))) & 255u;
+}
+
+// Record header checks shared by both paths: -1001 when the record does not
+// fit the stream, -91 for an impossible length.
+__device__ __forceinline__ int header_status(int64_t clen, int64_t avail, bool last, uint32_t maxlen) {
+    if (avail < 4 || clen == 0) return -1000 - 1;  // clen 0: LZ4's srcSize == 0 -> -1
+    if (clen < 0 || clen > (int64_t)maxlen || clen + 4 > avail || (!last && clen + 4 != avail))
+        return (clen + 4 > avail) ? -1000 - 1 : -91;
+    return 0;
+}
+
+// Byte reader of the scan: the lane's register window.
+struct GReader {
+    GWin g;
+    const uint8_t* P;
+    int clen;
+    __device__ __forceinline__ uint32_t operator()(int p) { return gw_byte(g, P, clen, p); }
+};
+
+// status[k] = number of sequences, or the block's final error code (r - 1000
+// for an LZ4 failure, -91 when the block does not decode to exactly n bytes).
+// seq[offs[k]/3 + i] = payload position of sequence i's token (a sequence
+// takes >= 3 record bytes, so the per-block ranges are disjoint).
+__global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= nb) return;
+    const int m = k < a.L.nfull ? a.L.bs : a.L.last;
+    const int n = m * a.L.E;
+    int64_t o0 = (int64_t)a.offs[k];
+    int64_t o1 = (k + 1 < nb) ? (int64_t)a.offs[k + 1] : o0 + 4 + (int64_t)a.maxlen;
+    if (o1 > a.in_nbytes) o1 = a.in_nbytes;
+    if (o0 > o1) o0 = o1;
+    const int64_t avail = o1 - o0;
+    const int64_t clen = avail >= 4 ? (int64_t)(int32_t)be32_global(a.in + o0) : 0;
+    int64_t st = header_status(clen, avail, k + 1 == nb, a.maxlen);
+    if (st == 0) {
+        int cnt = 0;
+        GReader rd;
+        rd.g.w0 = -(1 << 30);
+        rd.P = a.in + o0 + 4;
+        rd.clen = (int)clen;
+        const int r = scan_block(rd, (int)clen, n, a.seq + o0 / 3, cnt);
+        st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
+    }
+    a.status[k] = st;
+}
+
+// Returns this lane's token position of the record (two-phase path).
+__device__ __forceinline__ uint32_t land_record(const PayRegs& R, bool in_regs, const DecArgs& a,
+                                                const Span& sp, lds8* Cbuf, int lane) {
+    if (in_regs) {
+        land_pay(R, a, sp, Cbuf, lane);
+        return R.pos;
+    }
+    const gbl128c* g4 = span_base(a, sp);
+    const int nch = span_chunks(a, sp);
+    for (int c = lane; c < nch; c += kWave) ((lds128*)Cbuf)[c] = g4[c];
+    return a.seq[sp.o0 / 3 + lane];
+}
+
+// Persistent: workgroup w decodes blocks w, w+G, ...  Software pipeline, per
+// iteration: parse block i; land record i+1 (its loads were issued one whole
+// parse earlier); issue the offsets of i+3 and the record of i+2; store block
+// i.  Every wait on HBM therefore follows a parse, so neither load latency nor
+// the completion of the previous block's stores (gfx9 counts loads and stores
+// on one in-order vmcnt) stalls the wave.
 template <int EK, int VAR>
 __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -518,60 +526,60 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
 
-    Span cur = span_of(a, blk, nb);
-    Span nxt = {0, 0};
-    if (blk + stride < nb) nxt = span_of(a, blk + stride, nb);
     PayRegs R;
-    bool cur_in_regs = span_fits(a, cur);
-    if (cur_in_regs) issue_pay(R, a, cur, lane);
+    Span cur = span_from(a, issue_offs(a, blk, nb, lane));
+    uint32_t cur_pos;
+    {
+        const bool in_regs = span_fits(a, cur);
+        if (in_regs) issue_pay(R, a, cur, lane);
+        cur_pos = land_record(R, in_regs, a, cur, Cbuf, lane);
+    }
+    int64_t next = blk + stride;
+    Span nxt = {0, 0, 0};
+    bool nxt_in_regs = false;
+    if (next < nb) {
+        nxt = span_from(a, issue_offs(a, next, nb, lane));
+        nxt_in_regs = span_fits(a, nxt);
+        if (nxt_in_regs) issue_pay(R, a, nxt, lane);
+    }
+    OffRegs O{0, true};
+    if (next + stride < nb) O = issue_offs(a, next + stride, nb, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 
     for (;;) {
         const int m = blk < a.L.nfull ? a.L.bs : a.L.last;
-        const int n = m * E;
         const int P = m / 8;
-        // land this record in LDS
-        if (cur_in_regs) {
-            land_pay(R, a, cur, Cbuf, lane);
-        } else {
-            const gbl128c* g4 = span_base(a, cur);
-            const int nch = span_chunks(a, cur);
-            for (int c = lane; c < nch; c += kWave) ((lds128*)Cbuf)[c] = g4[c];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // prefetch: next record into registers, the one after into `nxt2`
-        const int64_t next = blk + stride;
-        const bool next_in_regs = next < nb && span_fits(a, nxt);
-        if (next_in_regs) issue_pay(R, a, nxt, lane);
-        Span nxt2 = {0, 0};
-        if (next + stride < nb) nxt2 = span_of(a, next + stride, nb);
-
-        const lds8* C = Cbuf + span_shift(a, cur);
-        const int avail = (int)(cur.o1 - cur.o0);
+        const int cp = span_shift(a, cur);
+        const lds8* C = Cbuf + cp;
+        // the scan's verdict: sequence count, or the block's error code
         int status = 0, clen = 0;
-        if (avail < 4) {
-            status = -1000 - 1;
+        if (cur.scan < 0) {
+            status = (int)cur.scan;
         } else {
             clen = (int)(((uint32_t)C[0] << 24) | ((uint32_t)C[1] << 16) | ((uint32_t)C[2] << 8) | C[3]);
-            const bool last = blk + 1 == nb;
-            if (clen <= 0 || (uint32_t)clen > a.maxlen || clen + 4 > avail ||
-                (!last && clen + 4 != avail))
-                status = (clen + 4 > avail) ? -1000 - 1 : -91;
-        }
-        if (status == 0) {
-            const int r = (VAR & 64) ? 0
-                          : (VAR & 2) ? lz4_decode_block_v2(C + 4, clen, a.ccap - 4, D, n, lane)
-                                      : lz4_decode_block<VAR>(C + 4, clen, D, n, lane);
-            status = (r == -91) ? -91 : (r < 0 ? r - 1000 : 0);
+            if (!(VAR & 64))
+                lz4_exec_block(Cbuf, cp + 4, D, a.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        // the next record replaces this one in LDS; then the loads two ahead
+        const int64_t nn = next + stride;
+        Span nxt2 = {0, 0, 0};
+        bool nxt2_in_regs = false;
+        uint32_t nxt_pos = 0;
+        if (next < nb) {
+            nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
+            if (nn < nb) {
+                nxt2 = span_from(a, O);
+                if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                nxt2_in_regs = span_fits(a, nxt2);
+                if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
+            }
+        }
         if (status == 0 && !(VAR & 8)) {
             uint8_t* dst = a.out + blk * (int64_t)a.L.bs * E;
             if constexpr (EK != 0) {
-              if ((VAR & 4) && (P & 3) == 0) {
-                untranspose_x4<EK>(D, dst, P, lane);
-              } else {
                 for (int g = lane; g < P; g += kWave) {
                     uint32_t w[2 * EK];
 #pragma unroll
@@ -585,7 +593,6 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                     }
                     store_group<EK>(dst + (int64_t)g * 8 * EK, w);
                 }
-              }
             } else {
                 for (int i = lane; i < P * E; i += kWave) {
                     const int g = i / E, b = i - g * E;
@@ -607,8 +614,10 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         if (next >= nb) break;
         blk = next;
         cur = nxt;
+        cur_pos = nxt_pos;
+        next = nn;
         nxt = nxt2;
-        cur_in_regs = next_in_regs;
+        nxt_in_regs = nxt2_in_regs;
     }
 }
 
@@ -698,35 +707,34 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15), 0};
+                  (int32_t)((nmax + 15) & ~15), nullptr};
         // decoded block + record (header, payload, 16-byte alignment slack)
         const size_t rec = (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
         const size_t lds = (size_t)a.cap + 16 + rec;
-        a.ccap = (int32_t)(rec - 16 - 8);  // record reads stay inside the buffer
         const bool aligned = ((uintptr_t)out & 15) == 0;
         const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
-        // tuning_variant(): bit1 the 256-byte-window block decoder (v2), bit2
-        // the 4-groups-per-lane inverse transpose -- both measured slower than
-        // the defaults on MI355X and kept for A/B; bits 3-6 are ABLATIONS for
-        // timing only (wrong output): 8 no output stores, 16 no literal copy,
-        // 32 no match copy, 64 no LZ4.
-        const int var = tuning_variant();
+        a.seq = b.seq;
+        // tuning_variant() (elem_size 2 only) ABLATIONS for timing, wrong
+        // output: 8 no output stores, 64 no sequence execution
+        const int var = tuning_variant() & (8 | 64);
         const void* fn = nullptr;
+#define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
         switch (ek) {
-            case 1: fn = reinterpret_cast<const void*>(k_lz4_decode<1, 0>); break;
+            case 1: fn = BSHUF_DEC(1, 0); break;
             case 2:
-                switch (var) {
-#define BSHUF_DEC_VAR(v) case v: fn = reinterpret_cast<const void*>(k_lz4_decode<2, v>); break;
-                    BSHUF_DEC_VAR(2) BSHUF_DEC_VAR(4) BSHUF_DEC_VAR(6) BSHUF_DEC_VAR(8)
-                    BSHUF_DEC_VAR(16) BSHUF_DEC_VAR(32) BSHUF_DEC_VAR(48) BSHUF_DEC_VAR(64)
-                    BSHUF_DEC_VAR(72)
-#undef BSHUF_DEC_VAR
-                    default: fn = reinterpret_cast<const void*>(k_lz4_decode<2, 0>); break;
-                }
+                fn = var == 8 ? BSHUF_DEC(2, 8) : var == 64 ? BSHUF_DEC(2, 64)
+                   : var == 72 ? BSHUF_DEC(2, 72) : BSHUF_DEC(2, 0);
                 break;
-            case 4: fn = reinterpret_cast<const void*>(k_lz4_decode<4, 0>); break;
-            case 8: fn = reinterpret_cast<const void*>(k_lz4_decode<8, 0>); break;
-            default: fn = reinterpret_cast<const void*>(k_lz4_decode<0, 0>); break;
+            case 4: fn = BSHUF_DEC(4, 0); break;
+            case 8: fn = BSHUF_DEC(8, 0); break;
+            default: fn = BSHUF_DEC(0, 0); break;
+        }
+#undef BSHUF_DEC
+        {
+            ProfScope prof("k_seq_scan", s);
+            hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, a, nb);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
         }
         if (lds > 65536) {
             e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -9,12 +9,13 @@
 //  * search: the probe positions of one search are fixed in advance by the
 //    skip schedule (probe_offset), so 64 lanes probe 64 consecutive candidate
 //    positions at once.  The sequential semantics "read table, then insert
-//    this position" are kept by (1) reading all 64 old entries, (2) inserting
-//    all 64 tentatively and reading back -- a lane that does not read its own
-//    position shares its hash with another lane of the window, (3) resolving
-//    such groups so each lane's candidate is the latest EARLIER lane with the
-//    same hash, (4) taking the first matching lane by ballot, and (5) undoing
-//    the inserts of lanes after that match.
+//    this position" come from ONE returning LDS atomic per window
+//    (ds_mskor_rtn_b32 on the u16 table, ds_wrxchg_rtn_b32 on the u32 one):
+//    the LDS serialises same-entry lanes in lane order, so each lane gets the
+//    latest EARLIER lane's position or the table's.  The first matching lane
+//    wins by ballot, and the inserts of later lanes are undone.  The lane-order
+//    property is checked on the device before first use; a device without it
+//    gets the insert/read-back/group-resolution window instead (VAR bit 128).
 //  * catch-up, match length (LZ4_count) and the 255-run length bytes are
 //    ballots over 64 byte/dword lanes.
 //  * the block (8 KiB by default) and the 16 KiB hash table live in LDS;
@@ -76,10 +77,6 @@ struct EncArgs {
     Layout L;
 };
 
-// The hash table, addressed explicitly in the LDS address space: a plain
-// volatile generic pointer compiles to flat_load/flat_store sc0 sc1, whose
-// vmcnt(0) waits would drain every outstanding global load and store.
-// volatile keeps the tentative insert -> read-back order of the search.
 // Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
 // asm waits for its own result, so the compiler never reads it early.
 __device__ __forceinline__ uint32_t lds_addr(void* p) {
@@ -98,6 +95,10 @@ __device__ __forceinline__ uint32_t lds_xchg_rtn(uint32_t addr, uint32_t data) {
     return r;
 }
 
+// The hash table, addressed explicitly in the LDS address space: a plain
+// volatile generic pointer compiles to flat_load/flat_store sc0 sc1, whose
+// vmcnt(0) waits would drain every outstanding global load and store.
+// volatile keeps the tentative insert -> read-back order of the fallback search.
 typedef __attribute__((address_space(3))) volatile uint16_t lds_vu16;
 typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 
@@ -258,7 +259,28 @@ struct EmitBytes {
         op += nb;
     }
     __device__ __forceinline__ void copy(int& op, const lds8* D, int from, int n) {
-        for (int i = lane; i < n; i += kWave) out[op + i] = D[from + i];
+        if (n <= kWave) {
+            if (lane < n) out[op + lane] = D[from + lane];
+        } else {
+            // long runs (the last literals above all): 16-byte stores to the
+            // ABSOLUTE 16-byte chunks inside the run, composed from five LDS
+            // dwords; the <= 15 bytes at each edge go byte-wise
+            const uintptr_t a0 = (uintptr_t)(out + op), a1 = a0 + (uintptr_t)n;
+            const uintptr_t q0 = (a0 + 15) & ~(uintptr_t)15, q1 = a1 & ~(uintptr_t)15;
+            const int head = (int)(q0 - a0), tailn = (int)(a1 - q1);
+            const int e = lane < 16 ? lane : n - tailn + (lane - 16);
+            if (lane < 16 ? lane < head : lane - 16 < tailn) out[op + e] = D[from + e];
+            const int nch = (int)((q1 - q0) >> 4);
+            for (int c = lane; c < nch; c += kWave) {
+                const int s = from + head + 16 * c;
+                const lds32* w = (const lds32*)(D + (s & ~3));
+                const uint32_t sh = (uint32_t)(s & 3);
+                const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+                *(gbl128*)(q0 + 16 * (uintptr_t)c) =
+                    u32x4{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                          __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+            }
+        }
         op += n;
     }
     __device__ __forceinline__ void finish(int) {}
@@ -275,6 +297,40 @@ struct CountOut {
     int tail_base;
     uint32_t tail;
 };
+
+// The re-test's match test and LZ4_count in one LDS round trip: counts the
+// equal bytes from ip itself (the first window's lane 0 is the 4-byte
+// test).  cnt = match length beyond kMinMatch, or -1 when there is no match.
+__device__ __forceinline__ CountOut test_and_count(const lds8* D, int n, int ip, int ref,
+                                                   int mlimit, int lane) {
+    CountOut r;
+    r.back = 0;
+    int pa = ip + 4 * lane, pb = ref + 4 * lane;
+    uint32_t va = lds_rd32(D, min(pa, n)), vb = lds_rd32(D, min(pb, n));
+    if (__builtin_amdgcn_readfirstlane(va ^ vb) != 0) {
+        r.cnt = -1;
+        return r;
+    }
+    int total = 0;
+    for (;;) {
+        const uint32_t x = va ^ vb;
+        int eq = x ? (__ffs(x) - 1) >> 3 : 4;
+        eq = min(eq, max(mlimit - pa, 0));
+        const uint64_t full = ballot(eq == 4);
+        if (full != ~0ull) {
+            const int f = ffs64(~full);
+            r.cnt = total + 4 * f + __builtin_amdgcn_readlane(eq, f) - kMinMatch;
+            r.tail_base = ip + total;
+            r.tail = va;
+            return r;
+        }
+        total += kWinBytes;
+        pa = ip + total + 4 * lane;
+        pb = ref + total + 4 * lane;
+        va = lds_rd32(D, min(pa, n));
+        vb = lds_rd32(D, min(pb, n));
+    }
+}
 
 __device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip, int ref,
                                                     int anchor, int mlimit, int lane) {
@@ -503,19 +559,24 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                 }
                 // the next search window's bytes, in flight during the re-test
                 pre = lds_rd32(D, min(ip + 1 + lane, n));
-                if (lane == 0) T.put(h2, (uint32_t)(ip - 2));
-                const uint32_t c2 = uni(T.get(h0));
-                if (lane == 0) T.put(h0, (uint32_t)ip);
+                uint32_t c2 = 0;
+                if (lane == 0) {
+                    T.put(h2, (uint32_t)(ip - 2));
+                    c2 = T.exchange(h0, (uint32_t)ip);
+                }
+                c2 = uni(c2);
                 const bool near = !WIDE || c2 + kMaxDistance >= (uint32_t)ip;
-                if (near && lds_rd32(D, (int)c2) == x0) {
-                    // zero-literal sequence, no catch-up on this path
-                    ref = (int)c2;
-                    co = catch_and_count(D, n, ip, ref, ip, mlimit, lane);
-                    mc = co.cnt;  // back == 0: anchor == ip
-                    em.byte(op, (uint32_t)(mc >= 15 ? 15 : mc));
-                    COUNT(3, 1);
-                    STAMP(4);
-                    continue;
+                if (near) {
+                    co = test_and_count(D, n, ip, (int)c2, mlimit, lane);
+                    if (co.cnt >= 0) {
+                        // zero-literal sequence, no catch-up on this path
+                        ref = (int)c2;
+                        mc = co.cnt;
+                        em.byte(op, (uint32_t)(mc >= 15 ? 15 : mc));
+                        COUNT(3, 1);
+                        STAMP(4);
+                        continue;
+                    }
                 }
                 STAMP(4);
                 break;

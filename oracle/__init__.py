@@ -156,6 +156,17 @@ class Reference(_Codec):
 
     def __init__(self, path=REF_SO):
         super().__init__(path, "bshuf_")
+        self.lib.LZ4_decompress_safe.restype = ctypes.c_int
+        self.lib.LZ4_decompress_safe.argtypes = [_c_void_p, _c_void_p, ctypes.c_int, ctypes.c_int]
+
+    def lz4_decompress_block(self, comp, capacity):
+        """LZ4 1.10.0's LZ4_decompress_safe (lz4/lz4.c:2451) on one raw block."""
+        comp = np.ascontiguousarray(comp, dtype=np.uint8)
+        out = np.empty(max(capacity, 1), dtype=np.uint8)
+        n = self.lib.LZ4_decompress_safe(_ptr(comp), _ptr(out), comp.size, capacity)
+        if n < 0:
+            raise RuntimeError("lz4 decode error %d" % n, n)
+        return out[:n].copy()
 
 
 def reference_available(path=REF_SO):

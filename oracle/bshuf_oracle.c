@@ -86,15 +86,23 @@ static int64_t blocked(orc_block_fn fn, const void* vin, void* vout, size_t n, s
     const size_t nfull = n / bs;
     size_t last = n % bs;
     last -= last % BLOCKED_MULT;
+    int64_t err = 0;
     for (size_t k = 0; k < nfull + (last ? 1 : 0); k++) {
         const size_t m = k < nfull ? bs : last;
         size_t c = 0, p = 0;
         const int64_t r = fn(in, out, m, E, &c, &p);
-        if (r < 0) return r;
-        total += r;
+        /* bshuf_blocked_wrap_fun (src/bitshuffle_core.c:1903-1917) keeps going
+         * and returns the error of the last failing block */
+        if (r < 0) {
+            err = r;
+            if (c == 0 && p == 0) return err; /* the chain cannot continue */
+        } else {
+            total += r;
+        }
         in += c;
         out += p;
     }
+    if (err < 0) return err;
     const size_t tail = (n % BLOCKED_MULT) * E;
     memcpy(out, in, tail);
     return total + (int64_t)tail;
@@ -268,50 +276,142 @@ last_literals: {
 /* LZ4 block decoder                                                   */
 /* ------------------------------------------------------------------ */
 
-int orc_lz4_decompress_block(const uint8_t* src, int csize, uint8_t* dst, int cap) {
-    const uint8_t* ip = src;
-    const uint8_t* const iend = src + csize;
-    uint8_t* op = dst;
-    uint8_t* const oend = dst + cap;
-    if (csize <= 0) return -1;
-    for (;;) {
-        if (ip >= iend) return -(int)(ip - src) - 1;
-        const unsigned tok = *ip++;
-        size_t lit = tok >> 4;
-        if (lit == 15) {
-            unsigned s;
-            do {
-                if (ip >= iend) return -(int)(ip - src) - 1;
-                s = *ip++;
-                lit += s;
-            } while (s == 255);
-        }
-        if ((size_t)(iend - ip) < lit || (size_t)(oend - op) < lit)
-            return -(int)(ip - src) - 1;
-        memcpy(op, ip, lit);
-        op += lit;
-        ip += lit;
-        if (ip == iend) break; /* last sequence: literals only */
-        if (iend - ip < 2) return -(int)(ip - src) - 1;
-        const size_t off = (size_t)ip[0] | ((size_t)ip[1] << 8);
-        ip += 2;
-        if (off == 0 || off > (size_t)(op - dst)) return -(int)(ip - src) - 1;
-        size_t ml = tok & 15;
-        if (ml == 15) {
-            unsigned s;
-            do {
-                if (ip >= iend) return -(int)(ip - src) - 1;
-                s = *ip++;
-                ml += s;
-            } while (s == 255);
-        }
-        ml += MINMATCH;
-        if ((size_t)(oend - op) < ml) return -(int)(ip - src) - 1;
-        const uint8_t* m = op - off;
-        for (size_t i = 0; i < ml; i++) op[i] = m[i]; /* overlap-safe, byte order */
-        op += ml;
+/* LZ4_decompress_safe of LZ4 1.10.0 (lz4/lz4.c:2022-2445 instantiated at
+ * 2451-2455: noDict, full block).  Its fast loop (2083-2209) and safe loop
+ * (2215-2435) check different margins, so both are restated to reproduce the
+ * same accept/reject decisions and error positions -(ip)-1.  Copies use byte
+ * semantics, which equal LZ4's wildcopies for every accepted stream (bytes a
+ * wildcopy writes past the sequence are rewritten before anything reads
+ * them); offset 0, which no compressor emits but the decoder accepts, copies
+ * zeros (the LZ4_write32(op, 0) seed of lz4.c:501 / 2407). */
+static int read_len(const uint8_t* src, int* ip, int ilimit, int initial_check, size_t* out) {
+    /* read_variable_length, lz4/lz4.c:1978-2014 */
+    if (initial_check && *ip >= ilimit) return -1;
+    unsigned s = src[(*ip)++];
+    size_t len = s;
+    if (*ip > ilimit) return -1;
+    while (s == 255) {
+        s = src[(*ip)++];
+        len += s;
+        if (*ip > ilimit) return -1;
     }
-    return (int)(op - dst);
+    *out = len;
+    return 0;
+}
+
+static void copy_match(uint8_t* dst, int64_t op, size_t off, size_t ml) {
+    if (off == 0) {
+        memset(dst + op, 0, ml);
+        return;
+    }
+    for (size_t i = 0; i < ml; i++) dst[op + (int64_t)i] = dst[op - (int64_t)off + (int64_t)i];
+}
+
+int orc_lz4_decompress_block(const uint8_t* src, int csize, uint8_t* dst, int cap) {
+    enum { E_NONE, E_LIT, E_COPY_MATCH, E_MATCH };
+    if (cap < 0) return -1;
+    if (cap == 0) return (csize == 1 && src[0] == 0) ? 0 : -1;
+    if (csize == 0) return -1;
+    const int64_t clen = csize, n = cap;
+    int ip = 0;
+    int64_t op = 0;
+    int fast = n >= 64; /* FASTLOOP_SAFE_DISTANCE */
+    for (;;) {
+        const unsigned tok = src[ip++];
+        size_t len = tok >> 4, ml = 0, off = 0, add = 0;
+        int entry = E_NONE;
+        if (fast) {
+            if (len == 15) {
+                if (read_len(src, &ip, (int)(clen - 15), 1, &add)) goto err;
+                len += add;
+                if (op + (int64_t)len > n - 32 || ip + (int64_t)len > clen - 32) entry = E_LIT;
+            } else if (ip > clen - 17) {
+                entry = E_LIT;
+            }
+            if (entry == E_NONE) {
+                memcpy(dst + op, src + ip, len);
+                ip += (int)len;
+                op += (int64_t)len;
+                off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
+                ip += 2;
+                ml = tok & 15;
+                if (ml == 15) {
+                    if (read_len(src, &ip, (int)(clen - 4), 0, &add)) goto err;
+                    ml += add + MINMATCH;
+                    if (op + (int64_t)ml >= n - 64) entry = E_MATCH;
+                } else {
+                    ml += MINMATCH;
+                    if (op + (int64_t)ml >= n - 64) {
+                        entry = E_MATCH;
+                    } else if (off >= 8 && (int64_t)off <= op) {
+                        copy_match(dst, op, off, ml);
+                        op += (int64_t)ml;
+                        continue;
+                    }
+                }
+                if (entry == E_NONE) {
+                    if ((int64_t)off > op) goto err;
+                    copy_match(dst, op, off, ml);
+                    op += (int64_t)ml;
+                    continue;
+                }
+            }
+            fast = 0; /* the rest of the block runs in the safe loop */
+        } else {
+            if (len != 15 && ip < clen - 16 && op <= n - 32) {
+                memcpy(dst + op, src + ip, len);
+                ip += (int)len;
+                op += (int64_t)len;
+                ml = tok & 15;
+                off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
+                ip += 2;
+                if (ml != 15 && off >= 8 && (int64_t)off <= op) {
+                    copy_match(dst, op, off, ml + MINMATCH);
+                    op += (int64_t)ml + MINMATCH;
+                    continue;
+                }
+                entry = E_COPY_MATCH;
+            } else {
+                if (len == 15) {
+                    if (read_len(src, &ip, (int)(clen - 15), 1, &add)) goto err;
+                    len += add;
+                }
+                entry = E_LIT;
+            }
+        }
+        if (entry == E_LIT) {
+            const int64_t cpy = op + (int64_t)len;
+            if (cpy > n - MFLIMIT || ip + (int64_t)len > clen - 8) {
+                /* must be the last sequence: consume the input exactly */
+                if (ip + (int64_t)len != clen || cpy > n) goto err;
+                memcpy(dst + op, src + ip, len);
+                op = cpy;
+                break;
+            }
+            memcpy(dst + op, src + ip, len);
+            ip += (int)len;
+            op = cpy;
+            off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
+            ip += 2;
+            ml = tok & 15;
+            entry = E_COPY_MATCH;
+        }
+        if (entry == E_COPY_MATCH) {
+            if (ml == 15) {
+                if (read_len(src, &ip, (int)(clen - 4), 0, &add)) goto err;
+                ml += add;
+            }
+            ml += MINMATCH;
+        }
+        /* safe_match_copy */
+        if ((int64_t)off > op) goto err;
+        if (op + (int64_t)ml > n - LASTLITERALS) goto err;
+        copy_match(dst, op, off, ml);
+        op += (int64_t)ml;
+    }
+    return (int)op;
+err:
+    return -ip - 1;
 }
 
 /* ------------------------------------------------------------------ */
@@ -353,10 +453,16 @@ static int64_t comp_block(const uint8_t* in, uint8_t* out, size_t m, size_t E, s
     return nb + 4;
 }
 
+/* bshuf_decompress_lz4_block (src/bitshuffle.c:83-119): the next record and
+ * output block are set from the header BEFORE decoding (lines 93-99), so a
+ * failing block does not stop the chain; its output is left untouched. */
 static int64_t decomp_block(const uint8_t* in, uint8_t* out, size_t m, size_t E, size_t* c,
                             size_t* p) {
     const int32_t nb = (int32_t)get_be32(in);
-    uint8_t* tmp = (uint8_t*)malloc(m * E);
+    if (nb < 0) return -1 - 1000; /* a negative size walks backwards: not followed */
+    *c = (size_t)nb + 4;
+    *p = m * E;
+    uint8_t* tmp = (uint8_t*)malloc(m * E ? m * E : 1);
     if (!tmp) return -1;
     const int r = orc_lz4_decompress_block(in + 4, nb, tmp, (int)(m * E));
     if (r < 0) {
@@ -369,8 +475,6 @@ static int64_t decomp_block(const uint8_t* in, uint8_t* out, size_t m, size_t E,
     }
     orc_untrans_bit_elem(tmp, out, m, E);
     free(tmp);
-    *c = (size_t)nb + 4;
-    *p = m * E;
     return nb + 4;
 }
 

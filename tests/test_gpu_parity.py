@@ -120,28 +120,96 @@ def test_lz4_matches_oracle(bs, oracle, kind):
                 assert back.tobytes() == arr.tobytes(), (kind, E, n, block)
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 6])
-def test_alternate_kernel_paths_match_oracle(bs, oracle, variant):
-    """The selectable non-default paths (elem_size 2): 128 = encoder
-    insert/readback search window (the fallback when the LDS-atomic lane-order
-    self-check fails); 2 = 256-byte-window block decoder; 4 = 4-groups-per-lane
-    inverse transpose; 6 = both."""
-    rng = np.random.default_rng(variant)
+def _with_variant(bs, variant, fn):
+    try:
+        bs.lib.bshuf_set_variant(variant)
+        return fn()
+    finally:
+        bs.lib.bshuf_set_variant(0)
+
+
+def test_encoder_fallback_search_matches_oracle(bs, oracle):
+    """Variant 128 selects (elem_size 2) the encoder's insert/read-back search
+    window: the fallback when the LDS-atomic lane-order self-check fails."""
+    rng = np.random.default_rng(128)
     cases = [oracle.gen_g1(3 * 4096 + 1005),
              (rng.integers(-2, 3, 50000).cumsum() % 97).astype(np.int16),
              np.repeat(rng.integers(0, 4, 9000), 7).astype(np.int16),
              rng.integers(0, 1 << 16, 20000).astype(np.uint16)]
-    try:
-        bs.lib.bshuf_set_variant(variant)
+
+    def run():
         for arr in cases:
             for block in [0, 64, 2048]:
                 want = oracle.compress_lz4(arr, block)
                 got = bs.compress_lz4(arr, block)
-                assert got.tobytes() == want.tobytes(), (variant, arr.size, block)
+                assert got.tobytes() == want.tobytes(), (arr.size, block)
                 back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
-                assert back.tobytes() == arr.tobytes(), (variant, arr.size, block)
-    finally:
-        bs.lib.bshuf_set_variant(0)
+                assert back.tobytes() == arr.tobytes(), (arr.size, block)
+    _with_variant(bs, 128, run)
+
+
+def _record(payload):
+    return np.frombuffer(len(payload).to_bytes(4, "big") + bytes(payload), dtype=np.uint8)
+
+
+# corrupt single-block payloads (4096 x u8, or 2048 x u16); each hits one
+# LZ4_decompress_safe check at a specific position
+_BAD_PAYLOADS = {
+    "litlen_run_to_end": [0xF0, 255, 255, 255],
+    "litlen_run_to_end_long": [0xF0] + [255] * 70,
+    "matchlen_run_to_end": [0x1F, 7, 1, 0, 255, 255],
+    "matchlen_run_to_end_long": [0x1F, 7, 1, 0] + [255] * 80,
+    "offset_zero": [0x10, 7, 0, 0, 0x00],
+    "offset_past_start": [0x20, 7, 8, 3, 0, 0x00],
+    "literals_truncated": [0x50, 1, 2],
+    "offset_truncated": [0x10, 7, 1],
+    "output_short": [0x30, 1, 2, 3],
+    "match_past_end": [0x1F, 7, 1, 0, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+                       255, 255, 255, 255, 255, 255, 100, 0x00],
+    "literals_past_end": [0xF0, 255] * 1 + [255] * 16 + [10] + [0] * 8,
+    "empty_token_run": [0x00, 1, 0],
+}
+
+
+@pytest.mark.parametrize("name", sorted(_BAD_PAYLOADS))
+def test_decompress_error_codes_match_oracle(bs, oracle, name):
+    """The error code of a corrupt record equals the oracle's (r - 1000 with r
+    LZ4_decompress_safe's -(position)-1, or -91)."""
+    for dtype, n in [(np.uint8, 4096), (np.uint16, 2048)]:
+        buf = _record(_BAD_PAYLOADS[name])
+        with pytest.raises(RuntimeError) as want:
+            oracle.decompress_lz4(buf, (n,), dtype)
+        with pytest.raises(RuntimeError) as got:
+            bs.decompress_lz4(buf, (n,), dtype)
+        assert got.value.args[1] == want.value.args[1], (name, dtype)
+
+
+def test_decompress_corrupt_blocks_match_oracle(bs, oracle):
+    """Seeded corruptions of valid LZ4 blocks (tests/test_oracle.py pins the
+    oracle's LZ4_decompress_safe restatement to the compiled reference on the
+    same generator): the GPU accepts exactly what the oracle accepts, with the
+    same output, and rejects the rest with the same error code."""
+    from tests.test_oracle import corrupt_lz4_blocks
+    checked = 0
+    for comp, cap in corrupt_lz4_blocks(oracle, seed=23, per_base=12):
+        # (records longer than LZ4_compressBound(block) -- no compressor emits
+        # one -- are rejected with -91 by design, see DESIGN.md)
+        if cap == 0 or cap % 8 or cap > 8192 or comp.size > cap + cap // 255 + 16:
+            continue
+        buf = _record(comp)
+        try:
+            want = ("ok", oracle.decompress_lz4(buf, (cap,), np.uint8).tobytes())
+        except RuntimeError as e:
+            want = ("err", e.args[1])
+        try:
+            got = ("ok", bs.decompress_lz4(buf, (cap,), np.uint8).tobytes())
+        except RuntimeError as e:
+            got = ("err", e.args[1])
+        assert got == want, (comp.size, cap, got[0], want[0],
+                             got[1] if got[0] == "err" else None,
+                             want[1] if want[0] == "err" else None)
+        checked += 1
+    assert checked > 300
 
 
 def test_lz4_u32_table_path(bs, oracle):

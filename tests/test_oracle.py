@@ -118,3 +118,73 @@ def test_oracle_vs_compiled_reference(oracle):
                 assert oracle.bitshuffle(arr, block).tobytes() == ref.bitshuffle(arr, block).tobytes()
                 assert oracle.compress_lz4(arr, block).tobytes() == \
                     ref.compress_lz4(arr, block).tobytes()
+
+
+def _lz4_outcome(codec, comp, cap):
+    try:
+        return ("ok", codec.lz4_decompress_block(comp, cap).tobytes())
+    except RuntimeError as e:
+        return ("err", e.args[1])
+
+
+def corrupt_lz4_blocks(oracle, seed=11, per_base=40):
+    """Valid LZ4 blocks of assorted sizes plus seeded corruptions of them:
+    random bytes, 0/15/255 bytes, truncations, extensions."""
+    rng = np.random.default_rng(seed)
+    bases = []
+    for n in [16, 40, 63, 64, 65, 80, 100, 300, 1000, 4096, 8192]:
+        for kind in range(4):
+            if kind == 0:
+                d = rng.integers(0, 256, n, dtype=np.uint8)
+            elif kind == 1:
+                d = np.repeat(rng.integers(0, 3, n // 5 + 1), 5)[:n].astype(np.uint8)
+            elif kind == 2:
+                d = (rng.integers(-1, 2, n).cumsum() % 7).astype(np.uint8)
+            else:
+                d = np.zeros(n, dtype=np.uint8)
+                d[rng.integers(0, n, max(n // 50, 1))] = rng.integers(0, 256, max(n // 50, 1))
+            bases.append((d, oracle.lz4_compress_block(d)))
+    cases = []
+    for d, c in bases:
+        n = d.size
+        cases.append((c, n))
+        cases.append((c, n + 1))
+        cases.append((c, max(n - 1, 0)))
+        for _ in range(per_base):
+            x = c.copy()
+            kind = rng.integers(0, 6)
+            if kind <= 2 and x.size:
+                k = int(rng.integers(1, 4))
+                idx = rng.integers(0, x.size, k)
+                x[idx] = [rng.integers(0, 256), 255, 0x0F, 0xF0, 0][kind] if kind else \
+                    rng.integers(0, 256, k)
+            elif kind == 3 and x.size > 1:
+                x = x[:int(rng.integers(1, x.size))]
+            elif kind == 4:
+                x = np.concatenate([x, rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8)])
+            else:
+                x = rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8)
+            cases.append((x, n))
+    return cases
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle",
+                                                    "_ref", "libbshuf_ref.so")),
+                    reason="oracle/_ref not built (needs /root/reference)")
+def test_lz4_decoder_matches_reference_on_corrupt_blocks(oracle):
+    """Pins the oracle's LZ4_decompress_safe restatement (accept/reject,
+    error position, output) against the compiled reference, on valid blocks
+    and ~1900 seeded corruptions of them."""
+    from oracle import Reference
+    ref = Reference()
+    diffs = []
+    cases = corrupt_lz4_blocks(oracle)
+    nerr = 0
+    for comp, cap in cases:
+        a, b = _lz4_outcome(oracle, comp, cap), _lz4_outcome(ref, comp, cap)
+        nerr += a[0] == "err"
+        if a != b:
+            diffs.append((comp.size, cap, a[0], a[1] if a[0] == "err" else len(a[1]),
+                          b[0], b[1] if b[0] == "err" else len(b[1])))
+    assert not diffs, diffs[:10]
+    assert nerr > len(cases) // 3  # the corruptions do exercise the error paths
