@@ -83,6 +83,8 @@ typedef __attribute__((address_space(3))) uint16_t lds16;
 typedef __attribute__((address_space(3))) uint32_t lds32;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds128;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds64v;
 __device__ __forceinline__ u32x4 vec4(const uint4& v) { return u32x4{v.x, v.y, v.z, v.w}; }
 
 __device__ __forceinline__ lds8* to_lds(void* p) { return (lds8*)(p); }

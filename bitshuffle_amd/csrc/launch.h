@@ -22,8 +22,12 @@ class ProfScope {
     void* a_;
 };
 
-// Kernel-variant knob for A/B measurements (bshuf_set_variant); 0 = default.
+// Kernel-variant knob for A/B measurements (bshuf_set_variant, per thread,
+// byte-identical variants only); 0 = default.
 int tuning_variant();
+#ifdef BSHUF_DIAG
+int diag_variant();  // timing ablations (wrong output), diag build only
+#endif
 
 // Workgroups for a persistent launch: resident blocks per CU (occupancy API,
 // dynamic LDS included) x CUs of the current device, capped by the work.

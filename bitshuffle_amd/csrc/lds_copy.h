@@ -1,0 +1,64 @@
+// lds_copy.h -- wave-level LDS byte-movement helpers shared by the LZ4 encoder
+// (sequence emission into the record staging buffer) and decoder (literal and
+// match execution).  All buffers are LDS (address space 3), 4-aligned bases.
+#pragma once
+
+#include "bshuf_dev.h"
+
+namespace bshuf {
+
+// One lane copies n <= 16 bytes (from a buffer with >= 16 readable bytes past
+// sp, or whose over-read stays inside LDS and is discarded).
+__device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int dp, int n) {
+    const lds32* w = (const lds32*)(S + (sp & ~3));
+    const uint32_t sh = (uint32_t)(sp & 3);
+    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+    const uint32_t v[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        if (i < n) Dd[dp + i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+}
+
+// The whole wave copies n bytes whose source ends at or before the
+// destination starts (or lies in another buffer).  Long runs go as aligned
+// destination dwords built from two source dwords, edges byte-wise.
+__device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int dp, int n, int lane) {
+    if (n <= kWave) {
+        if (lane < n) Dd[dp + lane] = S[sp + lane];
+        return;
+    }
+    const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
+    const int head = q0 - dp, tailn = dp + n - q1;
+    const int e = lane < 4 ? lane : n - tailn + (lane - 4);
+    if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn)) Dd[dp + e] = S[sp + e];
+    const int nw = (q1 - q0) >> 2;
+    for (int c = lane; c < nw; c += kWave) {
+        const int s2 = sp + head + 4 * c;
+        const lds32* w = (const lds32*)(S + (s2 & ~3));
+        ((lds32*)(Dd + q0))[c] = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(s2 & 3));
+    }
+}
+
+// Inclusive prefix sum over the 64 lanes (Hillis-Steele over __shfl_up).
+__device__ __forceinline__ int wave_incl_sum(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// LZ4 length continuation (lz4/lz4.c:1121-1130, 1205-1221): a length field
+// value v >= 15 is followed by (v-15)/255 bytes of 255 and one byte (v-15)%255.
+__host__ __device__ __forceinline__ int lz4_ext_bytes(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// Every lane writes its own continuation run of `cnt` bytes at p (cnt may be
+// 0): cnt-1 bytes of 255, then `last`.
+__device__ __forceinline__ void lane_len_run(lds8* S, int p, int cnt, uint32_t last) {
+    for (int i = 0; __builtin_amdgcn_ballot_w64(i < cnt) != 0; i++)
+        if (i < cnt) S[p + i] = (uint8_t)(i + 1 < cnt ? 255u : last);
+}
+
+}  // namespace bshuf

@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "launch.h"
+#include "lds_copy.h"
 #include "lz4_scan.h"
 
 namespace bshuf {
@@ -181,38 +182,6 @@ __global__ void k_idx_check(const uint64_t* base, int64_t nchunks, int64_t nbloc
 // each other (their sources end before the batch's first output byte).
 // ---------------------------------------------------------------------------
 
-// One lane copies n <= 16 bytes; S and Dd are 4-aligned LDS bases.
-__device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int dp, int n) {
-    const lds32* w = (const lds32*)(S + (sp & ~3));
-    const uint32_t sh = (uint32_t)(sp & 3);
-    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-    const uint32_t v[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-        if (i < n) Dd[dp + i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
-}
-
-// The whole wave copies n bytes whose source ends at or before the
-// destination starts (or lies in another buffer).  Long runs go as aligned
-// destination dwords built from two source dwords, edges byte-wise.
-__device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int dp, int n, int lane) {
-    if (n <= kWave) {
-        if (lane < n) Dd[dp + lane] = S[sp + lane];
-        return;
-    }
-    const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
-    const int head = q0 - dp, tailn = dp + n - q1;
-    const int e = lane < 4 ? lane : n - tailn + (lane - 4);
-    if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn)) Dd[dp + e] = S[sp + e];
-    const int nw = (q1 - q0) >> 2;
-    for (int c = lane; c < nw; c += kWave) {
-        const int s2 = sp + head + 4 * c;
-        const lds32* w = (const lds32*)(S + (s2 & ~3));
-        ((lds32*)(Dd + q0))[c] = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(s2 & 3));
-    }
-}
-
 // The whole wave runs a match that overlaps its own output (off < ml): the
 // output is periodic with period off.  Offset 0 (accepted by
 // LZ4_decompress_safe, never emitted by a compressor) writes zeros, as LZ4's
@@ -233,16 +202,6 @@ __device__ __forceinline__ void wave_fill(lds8* D, int op, int off, int ml, int 
             if (r >= off) r -= off;
         }
     }
-}
-
-// Inclusive prefix sum over the 64 lanes (Hillis-Steele over __shfl_up).
-__device__ __forceinline__ int wave_incl_sum(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int t = __shfl_up(v, d);
-        if (lane >= d) v += t;
-    }
-    return v;
 }
 
 // Phase 2 for one block.  The record payload starts at byte cp of the
@@ -714,16 +673,18 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
         const bool aligned = ((uintptr_t)out & 15) == 0;
         const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
         a.seq = b.seq;
-        // tuning_variant() (elem_size 2 only) ABLATIONS for timing, wrong
-        // output: 8 no output stores, 64 no sequence execution
-        const int var = tuning_variant() & (8 | 64);
         const void* fn = nullptr;
 #define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
         switch (ek) {
             case 1: fn = BSHUF_DEC(1, 0); break;
             case 2:
-                fn = var == 8 ? BSHUF_DEC(2, 8) : var == 64 ? BSHUF_DEC(2, 64)
-                   : var == 72 ? BSHUF_DEC(2, 72) : BSHUF_DEC(2, 0);
+                fn = BSHUF_DEC(2, 0);
+#ifdef BSHUF_DIAG
+                // diagnostic build only -- ABLATIONS for timing, wrong output:
+                // 8 no output stores, 64 no sequence execution
+                if (diag_variant() == 8) fn = BSHUF_DEC(2, 8);
+                if (diag_variant() == 64) fn = BSHUF_DEC(2, 64);
+#endif
                 break;
             case 4: fn = BSHUF_DEC(4, 0); break;
             case 8: fn = BSHUF_DEC(8, 0); break;

@@ -28,8 +28,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <atomic>
+#include <mutex>
 
 #include "launch.h"
+#include "lds_copy.h"
 
 namespace bshuf {
 
@@ -75,6 +77,8 @@ struct EncArgs {
     uint64_t* foot;
     int64_t slot;
     Layout L;
+    int32_t desc_ok;   // LDS holds kDescBytes of sequence descriptors at D + desc_off
+    int32_t desc_off;
 };
 
 // Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
@@ -141,112 +145,53 @@ __device__ __forceinline__ uint32_t hash_at(const lds8* D, int p) {
         return hash4(lds_rd32(D, p));
 }
 
+constexpr int kWinBytes = 4 * kWave;  // bytes one dword-per-lane wave access covers
+
 // ---------------------------------------------------------------------------
-// Output write-combining window.  Lane l holds output bytes
-// [base + 4l, base + 4l + 4) of a 256-byte window in a VGPR; tokens, length
-// bytes and offsets are bit-inserts into one lane, literals are 4-byte LDS
-// reads per lane, and a full window leaves as ONE coalesced 256-byte store.
-// (Byte-granular global stores would cost ~60x more store instructions and
-// stall the wave on its outstanding-VMEM limit.)
+// Emission policies of the parse.  The parse reports each sequence once its
+// match is final (seq) and the trailing literal run (last); `op` is the
+// running compressed size, kept by the parse in SGPRs.
+//
+//  * EmitDesc (default): the lane-0 store of an 8-byte descriptor into LDS;
+//    the LZ4 bytes are built afterwards by emit_sequences, wave-parallel, so
+//    literal copies and length runs are off the serial parse entirely.
+//  * EmitBytes: writes the bytes straight to global memory from inside the
+//    parse (blocks whose record does not fit the LDS staging area, the rare
+//    block with more sequences than descriptor slots, and the A/B variant 2).
 // ---------------------------------------------------------------------------
-struct OutWin {
-    uint32_t w;
-    int base;  // uniform, multiple of 256
-};
-
-constexpr int kWinBytes = 4 * kWave;
-
-__device__ __forceinline__ void ow_flush(OutWin& W, uint32_t* out32, int lane) {
-    out32[(W.base >> 2) + lane] = W.w;
-    W.base += kWinBytes;
+__device__ __forceinline__ int seq_bytes(int lit, int mc) {
+    return 3 + lz4_ext_bytes(lit) + lit + lz4_ext_bytes(mc);
 }
 
-// Byte mask of this lane's dword covering window-relative bytes [s, e).
-__device__ __forceinline__ uint32_t lane_mask(int lane, int s, int e) {
-    const int lo = 4 * lane;
-    const int a = max(s - lo, 0), b = min(e - lo, 4);
-    if (a >= b) return 0u;
-    const uint32_t hi = (b >= 4) ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
-    return hi & ~((1u << (8 * a)) - 1u);
-}
+constexpr int kDescMax = 256;              // descriptor slots per block
+constexpr int kDescBytes = 8 * kDescMax;   // LDS behind the block
 
-__device__ __forceinline__ void ow_byte(OutWin& W, uint32_t* out32, int& op, uint32_t b,
-                                        int lane) {
-    if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
-    const int rel = op - W.base;
-    if (lane == (rel >> 2)) {
-        const int sh = (rel & 3) * 8;
-        W.w = (W.w & ~(0xFFu << sh)) | (b << sh);
-    }
-    op++;
-}
-
-// LZ4 length continuation of v: v/255 bytes of 255, then v%255.
-__device__ __forceinline__ void ow_len(OutWin& W, uint32_t* out32, int& op, int v, int lane) {
-    int nb = v / 255 + 1;
-    const uint32_t rem = (uint32_t)(v - 255 * (nb - 1));
-    while (nb > 0) {
-        if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
-        const int rel = op - W.base;
-        const int take = min(nb, kWinBytes - rel);
-        const uint32_t m = lane_mask(lane, rel, rel + take);
-        W.w |= m;  // 0xFF bytes
-        if (take == nb) {
-            const int q = rel + take - 1;
-            if (lane == (q >> 2)) {
-                const int sh = (q & 3) * 8;
-                W.w = (W.w & ~(0xFFu << sh)) | (rem << sh);
-            }
-        }
-        op += take;
-        nb -= take;
-    }
-}
-
-// Copy D[from, from+len) (LDS) to the output stream at op.
-__device__ __forceinline__ void ow_copy(OutWin& W, uint32_t* out32, int& op, const lds8* D,
-                                        int from, int len, int lane) {
-    while (len > 0) {
-        if (op - W.base >= kWinBytes) ow_flush(W, out32, lane);
-        const int rel = op - W.base;
-        const int take = min(len, kWinBytes - rel);
-        const uint32_t m = lane_mask(lane, rel, rel + take);
-        const int p = from + 4 * lane - rel;  // source of this lane's first byte
-        const int pc = max(p, 0);             // p >= from - 3; lower bytes are masked
-        const uint32_t v = lds_rd32(D, pc) << (8 * (pc - p));
-        W.w = (W.w & ~m) | (v & m);
-        op += take;
-        from += take;
-        len -= take;
-    }
-}
-
-// Emission policies for lz4_encode_block: EmitWin (register window, one
-// coalesced store per 256 bytes) and EmitBytes (byte-granular stores).
-struct EmitWin {
-    OutWin W{0u, 0};
-    uint32_t* out32;
+struct EmitDesc {
+    lds32* desc;  // 2 dwords per sequence: ip | off << 16, lit | mc << 16
     int lane;
-    __device__ __forceinline__ void byte(int& op, uint32_t b) { ow_byte(W, out32, op, b, lane); }
-    __device__ __forceinline__ void len(int& op, int v) { ow_len(W, out32, op, v, lane); }
-    __device__ __forceinline__ void copy(int& op, const lds8* D, int from, int n) {
-        ow_copy(W, out32, op, D, from, n, lane);
+    int ns = 0;   // sequences recorded
+    int la = 0;   // anchor of the last literal run
+    __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
+        if (ns >= kDescMax) return false;
+        const int lit = ip - anchor;
+        if (lane == 0) {
+            ((lds64v*)desc)[ns] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
+                                        (uint32_t)lit | ((uint32_t)mc << 16)};
+        }
+        ns++;
+        op += seq_bytes(lit, mc);
+        return true;
     }
-    __device__ __forceinline__ void finish(int op) {
-        if (op > W.base) ow_flush(W, out32, lane);
+    __device__ __forceinline__ void last(int& op, int anchor, int n) {
+        la = anchor;
+        const int run = n - anchor;
+        op += 1 + lz4_ext_bytes(run) + run;
     }
-};
-
-// Ablation only (timing): emits nothing, same parse.
-struct EmitNone {
-    __device__ __forceinline__ void byte(int& op, uint32_t) { op++; }
-    __device__ __forceinline__ void len(int& op, int v) { op += v / 255 + 1; }
-    __device__ __forceinline__ void copy(int& op, const lds8*, int, int n) { op += n; }
-    __device__ __forceinline__ void finish(int) {}
 };
 
 struct EmitBytes {
     uint8_t* out;
+    const lds8* D_;  // the block (literal source)
     int lane;
     __device__ __forceinline__ void byte(int& op, uint32_t b) {
         if (lane == 0) out[op] = (uint8_t)b;
@@ -283,8 +228,63 @@ struct EmitBytes {
         }
         op += n;
     }
-    __device__ __forceinline__ void finish(int) {}
+    __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
+        const int lit = ip - anchor;
+        byte(op, (uint32_t)(((lit >= 15 ? 15 : lit) << 4) | (mc >= 15 ? 15 : mc)));
+        if (lit >= 15) len(op, lit - 15);
+        copy(op, D_, anchor, lit);
+        byte(op, (uint32_t)(off & 0xFF));
+        byte(op, (uint32_t)(off >> 8));
+        if (mc >= 15) len(op, mc - 15);
+        return true;
+    }
+    __device__ __forceinline__ void last(int& op, int anchor, int n) {
+        const int run = n - anchor;
+        byte(op, (uint32_t)((run >= 15 ? 15 : run) << 4));
+        if (run >= 15) len(op, run - 15);
+        copy(op, D_, anchor, run);
+    }
 };
+
+// Builds the LZ4 bytes of a parsed block from its descriptors, wave-parallel
+// (lane = sequence; a prefix sum places every sequence): record payload at
+// S[4..), literals from the block D.  The last literal run is sequence ns.
+__device__ void emit_sequences(const lds8* D, const lds32* desc, const int ns, const int la,
+                               const int n, lds8* S, const int lane) {
+    int opb = 4;
+    for (int b0 = 0; b0 <= ns; b0 += kWave) {
+        const int s = b0 + lane;
+        const bool m = s < ns;
+        const bool act = s <= ns;
+        int ip = n, off = 0, lit = act ? n - la : 0, mc = 0;
+        if (m) {
+            const u32x2 d = ((const lds64v*)desc)[s];
+            ip = (int)(d.x & 0xFFFFu);
+            off = (int)(d.x >> 16);
+            lit = (int)(d.y & 0xFFFFu);
+            mc = (int)(d.y >> 16);
+        }
+        const int le = lz4_ext_bytes(lit), me = m ? lz4_ext_bytes(mc) : 0;
+        const int len = act ? 1 + le + lit + (m ? 2 + me : 0) : 0;
+        const int incl = wave_incl_sum(len, lane);
+        const int op = opb + incl - len;
+        opb += __builtin_amdgcn_readlane(incl, kWave - 1);
+        if (act) S[op] = (uint8_t)((min(lit, 15) << 4) | (m ? min(mc, 15) : 0));
+        lane_len_run(S, op + 1, le, (uint32_t)(lit - 15) % 255u);
+        const int lp = op + 1 + le, lsrc = ip - lit;
+        if (lit > 0 && lit <= 16) lane_copy16(D, lsrc, S, lp, lit);
+        for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
+            const int l = ffs64(lm);
+            wave_copy(D, __builtin_amdgcn_readlane(lsrc, l), S, __builtin_amdgcn_readlane(lp, l),
+                      __builtin_amdgcn_readlane(lit, l), lane);
+        }
+        if (m) {
+            S[lp + lit] = (uint8_t)(off & 0xFF);
+            S[lp + lit + 1] = (uint8_t)(off >> 8);
+        }
+        lane_len_run(S, lp + lit + 2, me, (uint32_t)(mc - 15) % 255u);
+    }
+}
 
 // Catch-up (lz4/lz4.c:1105-1109) and LZ4_count (lz4/lz4.c:680-703) in one
 // LDS round trip: the match bytes [ip, ip+4) are equal, so counting from
@@ -388,10 +388,11 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(t & 3));
 }
 
-// Greedy LZ4 parse of D[0..n) with table T (zeroed); compressed bytes go to
-// out32 (4-byte aligned, room for the bound rounded up to 256).  Returns the
-// compressed size.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1,
-// notLimited output.
+// Greedy LZ4 parse of D[0..n) with table T (zeroed).  Every sequence goes to
+// em.seq() once its match is final, the trailing literal run to em.last().
+// Returns the compressed size, or -1 when the emitter ran out of descriptor
+// slots.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1, notLimited
+// output.
 template <bool WIDE, bool READBACK, class Emit>
 __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T, Emit& em,
                                 const int lane) {
@@ -526,20 +527,10 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
             int ref = mref - co.back;
             int mc = co.back + co.cnt;
             STAMP(1);
-            // ------------------------------------------------ emit sequence
-            {
-                const int lit = ip - anchor;
-                em.byte(op, (uint32_t)(((lit >= 15 ? 15 : lit) << 4) | (mc >= 15 ? 15 : mc)));
-                if (lit >= 15) em.len(op, lit - 15);
-                em.copy(op, D, anchor, lit);
-                COUNT(5, lit);
-            }
-            STAMP(2);
             for (;;) {
-                const int off = ip - ref;
-                em.byte(op, (uint32_t)(off & 0xFF));
-                em.byte(op, (uint32_t)(off >> 8));
-                if (mc >= 15) em.len(op, mc - 15);
+                // ------------------------------------------------ emit sequence
+                if (!em.seq(op, anchor, ip, ip - ref, mc)) return -1;
+                COUNT(5, ip - anchor);
                 ip += mc + kMinMatch;
                 anchor = ip;
                 STAMP(3);
@@ -572,7 +563,6 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                         // zero-literal sequence, no catch-up on this path
                         ref = (int)c2;
                         mc = co.cnt;
-                        em.byte(op, (uint32_t)(mc >= 15 ? 15 : mc));
                         COUNT(3, 1);
                         STAMP(4);
                         continue;
@@ -586,13 +576,7 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
         }
     }
     // ---------------------------------------------------- last literals
-    {
-        const int run = n - anchor;
-        em.byte(op, (uint32_t)((run >= 15 ? 15 : run) << 4));
-        if (run >= 15) em.len(op, run - 15);
-        em.copy(op, D, anchor, run);
-    }
-    em.finish(op);
+    em.last(op, anchor, n);
     STAMP(5);
     COUNT(4, 1);
     DIAG_FLUSH;
@@ -774,24 +758,41 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 
         uint8_t* out = a.scratch + blk * a.slot;
         const Table<WIDE> T{smem};
-        int c;
-        if constexpr ((VAR & 64) != 0) {
-            c = 0;  // ablation: transpose + table setup only
-        } else if constexpr ((VAR & 8) != 0) {
-            EmitNone em;
-            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
-        } else if constexpr ((VAR & 1) == 0) {
-            // default: byte-granular stores measured 11% faster than the
-            // register window (tools/ab.py, 2 GiB G1: 9.13 vs 10.29 ms)
-            EmitBytes em{out + 4, lane};
-            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
-        } else {
-            EmitWin em;
-            em.out32 = reinterpret_cast<uint32_t*>(out + 4);
-            em.lane = lane;
-            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
+        int c = -1;
+        // default: descriptors during the parse, bytes afterwards (the record
+        // is staged in the table's LDS, dead once the parse is over)
+        constexpr bool kDesc = !WIDE && (VAR & 2) == 0;
+        if constexpr (kDesc) {
+            if (a.desc_ok && 4 + lz4_bound(n) + 15 <= kTableBytes) {
+                lds32* desc = (lds32*)(D + a.desc_off);
+                EmitDesc em{desc, lane};
+                c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
+                if (c >= 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    lds8* S = to_lds(smem);
+                    emit_sequences(D, desc, em.ns, em.la, n, S, lane);
+                    if (lane < 4) S[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    const int nch = (4 + c + 15) >> 4;
+                    for (int i = lane; i < nch; i += kWave)
+                        ((gbl128*)out)[i] = ((const lds128*)S)[i];
+                } else {
+                    // more sequences than descriptor slots: parse again with
+                    // the inline emitter (fresh table)
+                    for (int i = lane; i < kTableBytes / 16; i += kWave)
+                        ((lds128*)to_lds(smem))[i] = u32x4{0u, 0u, 0u, 0u};
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
         }
-        if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
+        if (c < 0) {
+            EmitBytes em{out + 4, D, lane};
+            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
+            if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
+        }
         if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -889,47 +890,51 @@ __global__ __launch_bounds__(64) void k_lds_order_check(int* fails) {
     if (bad) atomicAdd(fails, bad);
 }
 
-// Once per device (cached): does k_lds_order_check pass?  Inside a stream
-// capture the check cannot run, and the encoder takes the readback path.
-bool lds_atomics_lane_ordered(hipStream_t s) {
+// Once per device (cached): does k_lds_order_check pass?  The check runs on a
+// private stream with a private (kept) allocation, so the caller's stream is
+// neither synchronised nor captured; its one hipStreamSynchronize happens on
+// the first encode per device.  Inside a caller's stream capture nothing of
+// this touches the captured stream.
+bool lds_atomics_lane_ordered() {
     static std::atomic<int> state[64];
+    static std::mutex mu;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    const int st = state[dev].load(std::memory_order_acquire);
+    int st = state[dev].load(std::memory_order_acquire);
     if (st) return st == 1;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return false;
+    std::lock_guard<std::mutex> g(mu);
+    st = state[dev].load(std::memory_order_acquire);
+    if (st) return st == 1;
+    hipStream_t ps = nullptr;
     int* d = nullptr;
     int h = -1;
-    bool ok = hipMalloc(&d, sizeof(int)) == hipSuccess;
-    ok = ok && hipMemsetAsync(d, 0, sizeof(int), s) == hipSuccess;
+    bool ok = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&d, sizeof(int)) == hipSuccess &&
+              hipMemsetAsync(d, 0, sizeof(int), ps) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(k_lds_order_check, dim3(1), dim3(kWave), 0, s, d);
+        hipLaunchKernelGGL(k_lds_order_check, dim3(1), dim3(kWave), 0, ps, d);
         ok = hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, s) == hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess;
+             hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, ps) == hipSuccess &&
+             hipStreamSynchronize(ps) == hipSuccess;
     }
-    if (d) (void)hipFree(d);
+    // d and ps are kept: freeing them could synchronise the device
     const bool ordered = ok && h == 0;
-    if (ok) state[dev].store(ordered ? 1 : 2, std::memory_order_release);
+    state[dev].store(ok ? (ordered ? 1 : 2) : 2, std::memory_order_release);
     return ordered;
 }
 
 template <int EK, bool WIDE, int VAR = 0>
 hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s) {
     if constexpr (EK == 2 && !WIDE && VAR == 0) {
-        // A/B + ablations (tools/ab.py, tools/ablate.py): 1 register-window
-        // emitter; 8 no output stores; 64 no LZ4 parse (timing only)
+        // byte-identical A/B variants (bshuf_set_variant, tools/ab.py): 2 inline
+        // emitter, 4 one-group-per-lane transpose, 128 insert/readback search
         const int v = tuning_variant();
-        if (v == 1) return launch_enc_t<2, false, 1>(a, nb, lds, s);
-        if (v == 8) return launch_enc_t<2, false, 8>(a, nb, lds, s);
-        if (v == 64) return launch_enc_t<2, false, 64>(a, nb, lds, s);
+        if (v == 2) return launch_enc_t<2, false, 2>(a, nb, lds, s);
         if (v == 4) return launch_enc_t<2, false, 4>(a, nb, lds, s);
-        if (v == 68) return launch_enc_t<2, false, 68>(a, nb, lds, s);
         if (v == 128) return launch_enc_t<2, false, 128>(a, nb, lds, s);
     }
-    if constexpr (VAR == 0) {  // (timing-only variants assume the property)
-        if (!lds_atomics_lane_ordered(s)) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
+    if constexpr ((VAR & 128) == 0) {
+        if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
     }
     auto fn = k_lz4_encode<EK, WIDE, VAR>;
     if (lds > 65536) {
@@ -967,10 +972,14 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
     const int64_t nb = L.nblocks();
     hipError_t e;
     if (nb > 0) {
-        EncArgs a{in, b.scratch, b.foot, b.slot, L};
         const int64_t nmax = (int64_t)L.bs * L.E;
-        const size_t lds = kTableBytes + ((nmax + 15) & ~15) + kDataPad;
         const bool wide = nmax >= kU16TableLimit;
+        // sequence descriptors behind the block when the record fits the
+        // table's LDS as staging (every block of up to ~16 KiB)
+        const bool desc = !wide && 4 + lz4_bound((int)nmax) + 15 <= kTableBytes;
+        const int32_t desc_off = (int32_t)(((nmax + 15) & ~15) + kDataPad);
+        EncArgs a{in, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off};
+        const size_t lds = kTableBytes + (size_t)desc_off + (desc ? kDescBytes : 0);
         // the partial block decides its own table type, so a stream whose full
         // blocks need byU32 but partial block byU16 launches twice
         const bool wide_last = L.last && (int64_t)L.last * L.E >= kU16TableLimit;

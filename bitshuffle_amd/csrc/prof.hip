@@ -52,8 +52,14 @@ Prof& P() {
 
 bool prof_on() { return P().on; }
 
-static int g_variant = 0;
-int tuning_variant() { return g_variant; }
+// A/B knob: per calling thread, and only byte-identical variants are accepted
+// (the timing ablations that change the output exist in the diag build only).
+static thread_local int t_variant = 0;
+int tuning_variant() { return t_variant; }
+#ifdef BSHUF_DIAG
+static int g_diag_variant = 0;
+int diag_variant() { return g_diag_variant; }
+#endif
 
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work) {
     int dev = 0, cus = 256, per = 1;
@@ -88,7 +94,17 @@ using namespace bshuf;
 
 extern "C" {
 
-void bshuf_set_variant(int v) { g_variant = v; }
+int bshuf_set_variant(int v) {
+    // 2 inline LZ4 emitter, 4 one-group-per-lane transpose, 128 insert/readback
+    // search window (the fallback for devices without lane-ordered LDS atomics)
+    if (v != 0 && v != 2 && v != 4 && v != 128) return -71;
+    t_variant = v;
+    return 0;
+}
+
+#ifdef BSHUF_DIAG
+void bshuf_diag_set_ablation(int v) { g_diag_variant = v; }
+#endif
 
 void bshuf_prof_enable(int on) {
     Prof& p = P();

@@ -73,9 +73,11 @@ int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first,
  * benchmarks: enable, run, then collect "name count total_ms" lines.
  * bshuf_prof_collect returns the buffer size needed and resets. */
 void bshuf_prof_enable(int on);
-/* Selects an alternative kernel variant for A/B measurements (0 = default;
- * every variant produces identical bytes). */
-void bshuf_set_variant(int v);
+/* Selects, for the CALLING THREAD only, an alternative kernel variant for A/B
+ * measurements: 0 default, 2 inline LZ4 emitter, 4 one-group-per-lane
+ * transpose, 128 insert/read-back search window.  Every accepted variant
+ * produces identical bytes; anything else is rejected with -71. */
+int bshuf_set_variant(int v);
 size_t bshuf_prof_collect(char* buf, size_t len);
 
 #ifdef __cplusplus

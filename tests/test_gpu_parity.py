@@ -122,15 +122,26 @@ def test_lz4_matches_oracle(bs, oracle, kind):
 
 def _with_variant(bs, variant, fn):
     try:
-        bs.lib.bshuf_set_variant(variant)
+        assert bs.lib.bshuf_set_variant(variant) == 0
         return fn()
     finally:
         bs.lib.bshuf_set_variant(0)
 
 
-def test_encoder_fallback_search_matches_oracle(bs, oracle):
-    """Variant 128 selects (elem_size 2) the encoder's insert/read-back search
-    window: the fallback when the LDS-atomic lane-order self-check fails."""
+def test_variant_knob_rejects_ablations(bs):
+    """Only byte-identical variants are accepted (and only for the calling
+    thread); timing ablations are not in the product library."""
+    for v in (1, 8, 64, 68, 3, -1):
+        assert bs.lib.bshuf_set_variant(v) == -71
+    assert bs.lib.bshuf_set_variant(0) == 0
+
+
+@pytest.mark.parametrize("variant", [128, 2, 4])
+def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
+    """Byte-identical alternate encoder paths (elem_size 2): 128 the insert/
+    read-back search window (the fallback when the LDS-atomic lane-order
+    self-check fails), 2 the inline emitter (also the overflow path of the
+    descriptor emitter), 4 the one-group-per-lane transpose."""
     rng = np.random.default_rng(128)
     cases = [oracle.gen_g1(3 * 4096 + 1005),
              (rng.integers(-2, 3, 50000).cumsum() % 97).astype(np.int16),
@@ -145,7 +156,7 @@ def test_encoder_fallback_search_matches_oracle(bs, oracle):
                 assert got.tobytes() == want.tobytes(), (arr.size, block)
                 back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
                 assert back.tobytes() == arr.tobytes(), (arr.size, block)
-    _with_variant(bs, 128, run)
+    _with_variant(bs, variant, run)
 
 
 def _record(payload):
@@ -292,8 +303,10 @@ def test_device_synth_matches_cpu_generators(bs, oracle, torch):
 # ------------------------------------------------------------------ full size
 @pytest.mark.slow
 def test_full_size_digests(bs, torch):
-    """BASELINE configs 1, 2 and 4 at full size vs SHA-256 of the reference's
-    output (tests/golden/vectors.json 'full'), plus decode round trips."""
+    """BASELINE configs 1-4 at full size vs SHA-256 of the reference's output
+    (tests/golden/vectors.json 'full'): the 64 MiB ramp, six 32 MiB chunks of
+    config 4, 4 GiB int16 G1 and 16 GiB float32 G2 (2**32 elements, a 6.9 GB
+    stream: > 2**31-element and > 4 GiB offsets), plus decode round trips."""
     import hashlib
     full = {e["name"]: e for e in load_vectors()["full"]}
 
@@ -313,10 +326,12 @@ def test_full_size_digests(bs, torch):
     assert torch.equal(bs.bitunshuffle_dev(y), x)
     del x, y
 
-    for name in ["cfg4_g1_chunk0000", "cfg4_g1_chunk1023", "cfg2_g1_i16_4GiB"]:
+    names = ["cfg4_g1_chunk%04d" % c for c in (0, 1, 2, 3, 511, 1023)]
+    for name in names + ["cfg2_g1_i16_4GiB", "cfg3_g2_f32_16GiB"]:
         e = full[name]
-        x = torch.empty(e["size"], dtype=torch.int16, device="cuda")
-        bs.synth_fill_dev(x, 1, seed=e.get("seed", 12345))
+        g2 = e["gen"] == "g2"
+        x = torch.empty(e["size"], dtype=torch.float32 if g2 else torch.int16, device="cuda")
+        bs.synth_fill_dev(x, 2 if g2 else 1, seed=e.get("seed", 12345))
         c = bs.compress_lz4_dev(x)
         assert c.numel() == e["compressed_len"], name
         assert digest(c) == e["compressed_sha256"], name

@@ -29,7 +29,7 @@ rd(buf)
 import bench  # noqa: E402
 prof = bench.prof_collect(B.lib)
 v = list(buf)
-names = ["search", "catchup", "literals", "matchcount", "retest+emit", "lastlit"]
+names = ["search", "catch+count", "(unused)", "seq-record", "retest", "last"]
 cnt = ["matches", "windows", "collision_windows", "retest_hits", "blocks", "literal_bytes",
        "searches"]
 blocks = max(v[12], 1)
