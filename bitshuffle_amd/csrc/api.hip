@@ -347,19 +347,29 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const
     // Walk the BE32 headers through the host buffer (the reference's own
     // iochain walk, src/bitshuffle.c:92-95) -- this also tells how many bytes
     // of `in` belong to the stream, which the caller does not pass.
+    // The walk stops at the first implausible header (length 0 or above
+    // LZ4_compressBound of its block): that record is staged up to the bound,
+    // the blocks behind it keep the all-ones "unresolved" offset, and the
+    // device decoder assigns every error code (-1001 / -91 / -1YYY), exactly
+    // as bshuf_decompress_lz4_dev does for the same bytes.
     const uint8_t* i8 = (const uint8_t*)in;
-    std::vector<uint64_t> offs((size_t)p.nb);
+    std::vector<uint64_t> offs((size_t)p.nb, ~(uint64_t)0);
     uint64_t pos = 0;
+    bool broken = false;
     for (int64_t k = 0; k < p.nb; k++) {
         offs[(size_t)k] = pos;
         const uint8_t* h = i8 + pos;
         const uint32_t len = ((uint32_t)h[0] << 24) | ((uint32_t)h[1] << 16) |
                              ((uint32_t)h[2] << 8) | h[3];
-        const int m = k < p.L.nfull ? p.L.bs : p.L.last;
-        if (len == 0 || len > (uint32_t)lz4_bound(m * p.L.E)) return -1000 - 1;
+        const uint32_t bound = (uint32_t)lz4_bound((k < p.L.nfull ? p.L.bs : p.L.last) * p.L.E);
+        if (len == 0 || len > bound) {
+            pos += 4 + (len ? (uint64_t)bound : 0);
+            broken = true;
+            break;
+        }
         pos += 4 + (uint64_t)len;
     }
-    const size_t in_nbytes = (size_t)pos + (size_t)p.tail;
+    const size_t in_nbytes = (size_t)pos + (broken ? 0 : (size_t)p.tail);
     const size_t bytes = size * elem_size;
     hipStream_t s = thread_stream();
     DevBuf di, dout, dres, doffs;

@@ -40,13 +40,19 @@ __device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int d
     }
 }
 
-// Inclusive prefix sum over the 64 lanes (Hillis-Steele over __shfl_up).
+// Inclusive prefix sum over the 64 lanes with DPP moves (no LDS round trip):
+// row_shr 1/2/4/8 scan each row of 16, row_bcast:15 carries row 0 into row 1
+// and row 2 into row 3, row_bcast:31 carries lanes 0-31 into rows 2-3.  Lanes
+// whose DPP source is outside the row read the `old` operand, 0.  All lanes
+// must be active.
 __device__ __forceinline__ int wave_incl_sum(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int t = __shfl_up(v, d);
-        if (lane >= d) v += t;
-    }
+    (void)lane;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
 }
 

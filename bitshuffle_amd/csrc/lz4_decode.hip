@@ -182,32 +182,85 @@ __global__ void k_idx_check(const uint64_t* base, int64_t nchunks, int64_t nbloc
 // each other (their sources end before the batch's first output byte).
 // ---------------------------------------------------------------------------
 
-// The whole wave runs a match that overlaps its own output (off < ml): the
-// output is periodic with period off.  Offset 0 (accepted by
-// LZ4_decompress_safe, never emitted by a compressor) writes zeros, as LZ4's
-// LZ4_write32(op, 0) seed makes it (lz4/lz4.c:501, 2407).
-__device__ __forceinline__ void wave_fill(lds8* D, int op, int off, int ml, int lane) {
-    const int s = op - off;
+// x mod d for 0 <= x < 2^24, d > 0, via the f32 reciprocal (one correction
+// step either way covers its rounding).
+__device__ __forceinline__ int small_mod(int x, int d, float rinv) {
+    const int q = (int)((float)x * rinv);
+    int r = x - q * d;
+    if (r < 0) r += d;
+    if (r >= d) r -= d;
+    return r;
+}
+
+// The whole wave runs one match D[mop, mop+ml) = LZ4 copy from mop-off.
+// Non-overlapping (off >= ml): a plain forward copy.  Overlapping (off < ml):
+// the output is periodic with period off, byte i = D[mop-off + i mod off], so
+// every byte reads the (final) bytes before the match and the interior goes
+// out as aligned dwords with no dependency on this match's own stores.
+// Offset 0 (accepted by LZ4_decompress_safe, never emitted by a compressor)
+// writes zeros, as LZ4's LZ4_write32(op, 0) seed makes it (lz4/lz4.c:501, 2407).
+__device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, int lane) {
+    if (off >= ml) {
+        wave_copy(D, mop - off, D, mop, ml, lane);
+        return;
+    }
     if (off == 0) {
-        for (int i = lane; i < ml; i += kWave) D[op + i] = 0;
-    } else if (off >= kWave) {
-        // every 64-byte chunk reads bytes written by earlier chunks
-        for (int i = lane; i < ml; i += kWave) D[op + i] = D[s + i];
-    } else {
-        int r = lane % off;
-        const int step = kWave % off;
-        for (int i = lane; i < ml; i += kWave) {
-            D[op + i] = D[s + r];
-            r += step;
-            if (r >= off) r -= off;
+        for (int i = lane; i < ml; i += kWave) D[mop + i] = 0;
+        return;
+    }
+    const int s = mop - off;
+    const float rinv = 1.0f / (float)off;
+    const int q0 = (mop + 3) & ~3, q1 = (mop + ml) & ~3;
+    if (q1 <= q0 || ml <= kWave) {
+        for (int i = lane; i < ml; i += kWave) D[mop + i] = D[s + small_mod(i, off, rinv)];
+        return;
+    }
+    // <= 3 head and <= 3 tail bytes, then the aligned interior dwords
+    const int head = q0 - mop, tailn = mop + ml - q1;
+    const int e = lane < 4 ? lane : ml - tailn + (lane - 4);
+    if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn))
+        D[mop + e] = D[s + small_mod(e, off, rinv)];
+    const int nw = (q1 - q0) >> 2;
+    const int step = small_mod(4 * kWave, off, rinv);
+    int r = small_mod(head + 4 * lane, off, rinv);
+    lds32* W = (lds32*)(D + q0);
+    for (int c = lane; c < nw; c += kWave) {
+        int r1 = r + 1;
+        r1 = r1 >= off ? r1 - off : r1;
+        int r2 = r1 + 1;
+        r2 = r2 >= off ? r2 - off : r2;
+        int r3 = r2 + 1;
+        r3 = r3 >= off ? r3 - off : r3;
+        W[c] = (uint32_t)D[s + r] | ((uint32_t)D[s + r1] << 8) | ((uint32_t)D[s + r2] << 16) |
+               ((uint32_t)D[s + r3] << 24);
+        r += step;
+        r = r >= off ? r - off : r;
+    }
+}
+
+// LZ4 length continuation starting at record byte q, whose next `av` bytes
+// (av <= 8) are already in w: returns the added length, advances q.
+__device__ __forceinline__ int read_ext(const lds8* Cb, int& q, uint64_t w, int av) {
+    int v = 0;
+    for (;;) {
+        uint64_t inv = ~w;
+        if (av < 8) inv &= (1ull << (8 * av)) - 1ull;
+        if (inv) {
+            const int k = (__ffsll((unsigned long long)inv) - 1) >> 3;
+            q += k + 1;
+            return v + 255 * k + (int)((w >> (8 * k)) & 255u);
         }
+        v += 255 * av;
+        q += av;
+        w = lds_rd64(Cb, q);
+        av = 8;
     }
 }
 
 // Phase 2 for one block.  The record payload starts at byte cp of the
 // 4-aligned LDS buffer Cb; pos[0..nseq) are its token positions (payload-
 // relative, validated by the scan); pos0 is this lane's prefetched pos[lane].
-__device__ void lz4_exec_block(const lds8* Cb, const int cp, lds8* D,
+__device__ __forceinline__ void lz4_exec_block(const lds8* Cb, const int cp, lds8* D,
                                const uint32_t* __restrict__ pos, const int nseq, uint32_t pos0,
                                const int lane) {
     int opb = 0;
@@ -217,33 +270,26 @@ __device__ void lz4_exec_block(const lds8* Cb, const int cp, lds8* D,
         const bool act = j < nseq;
         const int tp = act ? (int)pnext : 0;
         if (c0 + kWave < nseq && c0 + kWave + lane < nseq) pnext = pos[c0 + kWave + lane];
-        // ---- sequence fields, lane = sequence
+        // ---- sequence fields, lane = sequence: the token and the 7 bytes
+        // behind it in one read (a zero-literal sequence's offset and first
+        // length bytes are among them), else one more read at the offset
         const int p = cp + tp;
-        const uint32_t x = lds_rd32(Cb, p);
+        const uint64_t x = lds_rd64(Cb, p);
         const int tok = (int)(x & 255u);
         int lit = act ? tok >> 4 : 0;
         int q = p + 1;
-        if (lit == 15) {
-            int b;
-            do {
-                b = Cb[q++];
-                lit += b;
-            } while (b == 255);
-        }
+        if (lit == 15) lit += read_ext(Cb, q, x >> 8, 7);
         const int lsrc = q;
         q += lit;
         int off = 0, ml = 0;
         if (act && j + 1 < nseq) {  // the last sequence has no match
-            off = lit == 0 ? (int)((x >> 8) & 0xFFFFu) : (int)(lds_rd32(Cb, q) & 0xFFFFu);
+            const int d = q - p;    // bytes of x already behind q
+            const uint64_t y = d <= 6 ? x >> (8 * d) : lds_rd64(Cb, q);
+            const int yav = d <= 6 ? 8 - d : 8;
+            off = (int)(y & 0xFFFFu);
             q += 2;
             ml = tok & 15;
-            if (ml == 15) {
-                int b;
-                do {
-                    b = Cb[q++];
-                    ml += b;
-                } while (b == 255);
-            }
+            if (ml == 15) ml += read_ext(Cb, q, y >> 16, yav - 2);
             ml += kMinMatch;
         }
         const int len = lit + ml;
@@ -271,13 +317,8 @@ __device__ void lz4_exec_block(const lds8* Cb, const int cp, lds8* D,
             if (inb && !coop) lane_copy16(D, mop - off, D, mop, ml);
             for (uint64_t cm = ballot(coop); cm; cm &= cm - 1) {
                 const int l = ffs64(cm);
-                const int lo = __builtin_amdgcn_readlane(off, l);
-                const int lm = __builtin_amdgcn_readlane(ml, l);
-                const int lp = __builtin_amdgcn_readlane(mop, l);
-                if (lo >= lm)
-                    wave_copy(D, lp - lo, D, lp, lm, lane);
-                else
-                    wave_fill(D, lp, lo, lm, lane);
+                wave_match(D, __builtin_amdgcn_readlane(mop, l), __builtin_amdgcn_readlane(off, l),
+                           __builtin_amdgcn_readlane(ml, l), lane);
             }
             todo &= g >= kWave ? 0ull : (~0ull << g);
         }
@@ -296,6 +337,18 @@ struct DecArgs {
     int32_t cap;     // LDS bytes reserved for the decoded block
     uint32_t* seq;   // token positions (k_seq_scan -> lz4_exec_block)
 };
+
+// Record span [o0, o1) clamped into the stream: an offset the index could not
+// resolve (launch_index leaves it at the all-ones sentinel) or a corrupt one
+// becomes an empty span at the stream end, which the header check rejects
+// (-1001) without reading anything; a span never exceeds the largest record.
+__device__ __forceinline__ void clamp_span(int64_t& o0, int64_t& o1, int64_t in_nbytes,
+                                           uint32_t maxlen) {
+    if (o0 < 0 || o0 > in_nbytes) o0 = in_nbytes;
+    if (o1 < 0 || o1 > in_nbytes) o1 = in_nbytes;
+    if (o0 > o1) o0 = o1;
+    if (o1 > o0 + 4 + (int64_t)maxlen) o1 = o0 + 4 + (int64_t)maxlen;
+}
 
 // Byte range [o0, o1) of block k's record ([BE32 c][c bytes]) in the stream.
 // Consecutive records are contiguous, so the next offset ends this record;
@@ -382,8 +435,7 @@ __device__ __forceinline__ Span span_from(const DecArgs& a, const OffRegs& r) {
     sp.o0 = rl(0);
     sp.o1 = r.last ? sp.o0 + 4 + (int64_t)a.maxlen : rl(1);
     sp.scan = rl(2);
-    if (sp.o1 > a.in_nbytes) sp.o1 = a.in_nbytes;
-    if (sp.o0 > sp.o1) sp.o0 = sp.o1;
+    clamp_span(sp.o0, sp.o1, a.in_nbytes, a.maxlen);
     return sp;
 }
 
@@ -438,8 +490,7 @@ __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     const int n = m * a.L.E;
     int64_t o0 = (int64_t)a.offs[k];
     int64_t o1 = (k + 1 < nb) ? (int64_t)a.offs[k + 1] : o0 + 4 + (int64_t)a.maxlen;
-    if (o1 > a.in_nbytes) o1 = a.in_nbytes;
-    if (o0 > o1) o0 = o1;
+    clamp_span(o0, o1, a.in_nbytes, a.maxlen);
     const int64_t avail = o1 - o0;
     const int64_t clen = avail >= 4 ? (int64_t)(int32_t)be32_global(a.in + o0) : 0;
     int64_t st = header_status(clen, avail, k + 1 == nb, a.maxlen);
@@ -626,6 +677,10 @@ hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const De
     const int64_t nb = L.nblocks();
     hipError_t e = hipMemsetAsync(b.idx_err, 0, sizeof(int64_t), s);
     if (e != hipSuccess || nb == 0) return e;
+    // offsets a broken chain never reaches stay at the all-ones sentinel
+    // (clamp_span turns them into -1001 without reading the stream)
+    e = hipMemsetAsync(b.offs, 0xFF, (size_t)nb * sizeof(uint64_t), s);
+    if (e != hipSuccess) return e;
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     const int64_t W = 4 + (int64_t)maxlen;
     const int64_t nch = b.nchunks;
@@ -684,6 +739,7 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
                 // 8 no output stores, 64 no sequence execution
                 if (diag_variant() == 8) fn = BSHUF_DEC(2, 8);
                 if (diag_variant() == 64) fn = BSHUF_DEC(2, 64);
+                if (diag_variant() == 72) fn = BSHUF_DEC(2, 72);
 #endif
                 break;
             case 4: fn = BSHUF_DEC(4, 0); break;

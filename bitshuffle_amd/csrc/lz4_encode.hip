@@ -249,7 +249,7 @@ struct EmitBytes {
 // Builds the LZ4 bytes of a parsed block from its descriptors, wave-parallel
 // (lane = sequence; a prefix sum places every sequence): record payload at
 // S[4..), literals from the block D.  The last literal run is sequence ns.
-__device__ void emit_sequences(const lds8* D, const lds32* desc, const int ns, const int la,
+__device__ __forceinline__ void emit_sequences(const lds8* D, const lds32* desc, const int ns, const int la,
                                const int n, lds8* S, const int lane) {
     int opb = 4;
     for (int b0 = 0; b0 <= ns; b0 += kWave) {

@@ -249,6 +249,45 @@ def test_decompress_errors(bs, oracle):
         bs.decompress_lz4(enc[:-1], arr.shape, arr.dtype)  # consumed != buffer size
 
 
+def _block_header_positions(enc, nblocks):
+    pos, out = 0, []
+    for _ in range(nblocks):
+        out.append(pos)
+        pos += 4 + int.from_bytes(enc[pos:pos + 4].tobytes(), "big")
+    return out
+
+
+def test_device_decode_truncated_and_corrupt_headers(bs, oracle, torch):
+    """The device decoder WITHOUT block offsets (parallel index rebuild) on
+    truncated streams and on corrupted block headers: every read stays inside
+    in_nbytes and the call reports an error instead of decoding; where the
+    host drop-in path sees the same bytes (a corrupt last header) both return
+    the same code."""
+    a = oracle.gen_g1(20 * 4096 + 1000 + 3)
+    enc = oracle.compress_lz4(a)
+    nb = 21
+    hdr = _block_header_positions(enc, nb)
+    bad = [enc[:-1], enc[:hdr[7] + 2], enc[:hdr[12]], enc[:len(enc) // 2], enc[:3]]
+    for k, val in [(5, 0), (5, 0xFFFFFFFF), (5, None), (nb - 1, 0), (nb - 1, 9000)]:
+        e = enc.copy()
+        if val is None:  # off by one
+            val = int.from_bytes(e[hdr[k]:hdr[k] + 4].tobytes(), "big") + 1
+        e[hdr[k]:hdr[k] + 4] = np.frombuffer(int(val).to_bytes(4, "big"), dtype=np.uint8)
+        bad.append(e)
+    for i, buf in enumerate(bad):
+        t = torch.from_numpy(np.ascontiguousarray(buf)).cuda()
+        with pytest.raises(RuntimeError) as dev:
+            bs.decompress_lz4_dev(t, a.shape, torch.int16)
+        torch.cuda.synchronize()
+        if i >= len(bad) - 2:  # corrupt LAST header: host walk == device index
+            # (padded: like the reference, the host path reads up to the
+            # header's claimed record length, capped at the LZ4 bound)
+            padded = np.concatenate([buf, np.zeros(9000, dtype=np.uint8)])
+            with pytest.raises(RuntimeError) as host:
+                bs.decompress_lz4(padded, a.shape, a.dtype)
+            assert host.value.args[1] == dev.value.args[1], i
+
+
 # ------------------------------------------------------------------ device API
 def test_device_api_roundtrip_and_index(bs, oracle, torch):
     for spec in load_vectors()["small"]:
