@@ -13,6 +13,7 @@ Host (numpy) functions
     decompress_lz4(arr, shape, dtype, block_size=0) -> array
 Device (torch CUDA/HIP tensor) functions, no host round trip
     bitshuffle_dev / bitunshuffle_dev / compress_lz4_dev / decompress_lz4_dev
+    compress_lz4_batch_dev / decompress_lz4_batch_dev  (many streams per launch)
 """
 from ._lib import (  # noqa: F401
     LIB_PATH,
@@ -30,9 +31,11 @@ from .api import (  # noqa: F401
     bitunshuffle,
     bitunshuffle_dev,
     compress_lz4,
+    compress_lz4_batch_dev,
     compress_lz4_bound,
     compress_lz4_dev,
     decompress_lz4,
+    decompress_lz4_batch_dev,
     decompress_lz4_dev,
     default_block_size,
     synth_fill_dev,
@@ -56,4 +59,6 @@ __all__ = [
     "bitunshuffle_dev",
     "compress_lz4_dev",
     "decompress_lz4_dev",
+    "compress_lz4_batch_dev",
+    "decompress_lz4_batch_dev",
 ]

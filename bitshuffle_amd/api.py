@@ -203,6 +203,86 @@ def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None
     return out
 
 
+def _ptr_array(vals):
+    arr = (ctypes.c_void_p * len(vals))(*[ctypes.c_void_p(v) for v in vals])
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+def _size_array(vals):
+    arr = (ctypes.c_size_t * len(vals))(*vals)
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+def compress_lz4_batch_dev(tensors, block_size=0, outs=None, workspace=None, offsets=None,
+                           stream=None, sync=True):
+    """bshuf_compress_lz4_batch_dev over a list of device tensors (same dtype):
+    one launch per kernel for all of them.  Returns the list of framed uint8
+    streams (sync=True), or (outs, results) with results a device int64 tensor
+    of per-stream byte counts / error codes."""
+    torch = _torch()
+    if not tensors:
+        return []
+    es = tensors[0].element_size()
+    sizes = [t.numel() for t in tensors]
+    if outs is None:
+        outs = [torch.empty(max(compress_lz4_bound(n, es, block_size), 1), dtype=torch.uint8,
+                            device=t.device) for n, t in zip(sizes, tensors)]
+    for t in tensors:
+        if t.element_size() != es:
+            raise ValueError("all tensors of a batch need the same element size")
+        _dptr(t)
+    results = torch.empty(len(tensors), dtype=torch.int64, device=tensors[0].device)
+    pin, keep1 = _ptr_array([t.data_ptr() for t in tensors])
+    pout, keep2 = _ptr_array([o.data_ptr() for o in outs])
+    psz, keep3 = _size_array(sizes)
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    wsb = workspace.numel() if workspace is not None else 0
+    offp = _dptr(offsets) if offsets is not None else None
+    _check(lib.bshuf_compress_lz4_batch_dev(pin, pout, psz, len(tensors), es, block_size, ws, wsb,
+                                            _dptr(results), offp, _stream(stream)))
+    if not sync:
+        return outs, results
+    counts = results.cpu().tolist()
+    for c in counts:
+        if c < 0:
+            _fail(c)
+    return [o[:c] for o, c in zip(outs, counts)]
+
+
+def decompress_lz4_batch_dev(bufs, shapes, dtype, block_size=0, outs=None, workspace=None,
+                             stream=None, sync=True):
+    """bshuf_decompress_lz4_batch_dev: each uint8 device tensor of `bufs` is one
+    whole framed stream; returns the decoded tensors (sync=True), or (outs,
+    results) with per-stream consumed byte counts / error codes."""
+    torch = _torch()
+    if not bufs:
+        return []
+    if outs is None:
+        outs = [torch.empty(tuple(sh), dtype=dtype, device=b.device) for b, sh in zip(bufs, shapes)]
+    es = outs[0].element_size()
+    sizes = [o.numel() for o in outs]
+    nbytes = [b.numel() for b in bufs]
+    results = torch.empty(len(bufs), dtype=torch.int64, device=bufs[0].device)
+    pin, keep1 = _ptr_array([_dptr(b).value or 0 for b in bufs])
+    pout, keep2 = _ptr_array([_dptr(o).value or 0 for o in outs])
+    psz, keep3 = _size_array(sizes)
+    pnb, keep4 = _size_array(nbytes)
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    wsb = workspace.numel() if workspace is not None else 0
+    _check(lib.bshuf_decompress_lz4_batch_dev(pin, pnb, pout, psz, len(bufs), es, block_size, ws,
+                                              wsb, _dptr(results), _stream(stream)))
+    if not sync:
+        return outs, results
+    counts = results.cpu().tolist()
+    for c, nb in zip(counts, nbytes):
+        if c < 0:
+            _fail(c)
+        if c != nb:
+            raise BshufError("Decompressed different number of bytes than input buffer size."
+                             "Input buffer %d, decompressed %d." % (nb, c), c)
+    return outs
+
+
 def synth_fill_dev(t, gen, first=0, seed=12345, stream=None):
     """Fill tensor t with synthetic input G0 (int32 ramp), G1 (int16) or G2 (float32)."""
     _check(lib.bshuf_synth_fill_dev(_dptr(t), t.numel(), gen, first, seed, _stream(stream)))

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/bitshuffle.h"
@@ -261,6 +262,230 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
     }
     if (launch_decode(i8, (int64_t)in_nbytes, (uint8_t*)out, p.L, p.tail, b, d_result, s) !=
         hipSuccess)
+        return kErrHip;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// batched device entry points: `count` independent streams per launch
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct BatchPlan {
+    std::vector<Seg> segs;
+    Layout L;        // shared bs, E; L.nfull = total blocks
+    int64_t nb = 0;  // total blocks
+    int64_t nchunks = 0;
+    int64_t seq_words = 0;
+    int64_t chunk = 0;
+};
+
+// Segment table of a batch (src/bitshuffle_core.c:1877-1931 blocking per
+// stream); in_nbytes == nullptr for the encoder.
+int64_t make_batch(const void* const* in, void* const* out, const size_t* sizes,
+                   const size_t* in_nbytes, size_t count, size_t elem_size, size_t block_size,
+                   BatchPlan& bp) {
+    if (count == 0 || count > (size_t)INT32_MAX) return kErrUnsupported;
+    bp.segs.resize(count);
+    for (size_t i = 0; i < count; i++) {
+        Plan p;
+        const int64_t r = make_plan(sizes[i], elem_size, block_size, p);
+        if (r) return r;
+        if (i == 0) {
+            bp.L = p.L;
+            bp.chunk = index_chunk_bytes(p.L);
+        }
+        Seg& g = bp.segs[i];
+        g.in = in ? (const uint8_t*)in[i] : nullptr;
+        g.out = out ? (uint8_t*)out[i] : nullptr;
+        g.first = bp.nb;
+        g.nfull = p.L.nfull;
+        g.last = p.L.last;
+        g.pad_ = 0;
+        g.tail = p.tail;
+        g.in_nbytes = in_nbytes ? (int64_t)in_nbytes[i] : 0;
+        const int64_t cb = std::max<int64_t>(g.in_nbytes - g.tail, 0);
+        g.chunk0 = bp.nchunks;
+        g.nchunks = cb > 0 ? (cb + bp.chunk - 1) / bp.chunk : 0;
+        g.seq0 = bp.seq_words;
+        g.result = nullptr;
+        bp.nb += p.nb;
+        bp.nchunks += g.nchunks;
+        bp.seq_words += g.in_nbytes / 3 + 80;
+    }
+    if ((int64_t)bp.L.bs * bp.L.E > max_device_block_bytes()) return kErrUnsupported;
+    bp.L.nfull = bp.nb;
+    bp.L.last = 0;
+    return 0;
+}
+
+size_t enc_batch_ws(const BatchPlan& bp, EncodeBufs* b, Seg** dsegs, uint32_t** blk_seg,
+                    uint8_t* base) {
+    Carver c{base};
+    Seg* sg = c.take<Seg>(bp.segs.size() * sizeof(Seg));
+    uint32_t* bm = c.take<uint32_t>((size_t)bp.nb * 4 + 4);
+    EncodeBufs x;
+    x.slot = encode_slot_bytes(bp.L);
+    x.scratch = c.take<uint8_t>((size_t)(bp.nb * x.slot));
+    x.foot = c.take<uint64_t>((size_t)(bp.nb + 1) * 8);
+    x.offs = c.take<uint64_t>((size_t)(bp.nb + 1) * 8);
+    x.scan_tmp_bytes = encode_scan_tmp_bytes(bp.nb);
+    x.scan_tmp = c.take<void>(x.scan_tmp_bytes);
+    if (b) *b = x;
+    if (dsegs) *dsegs = sg;
+    if (blk_seg) *blk_seg = bm;
+    return c.off;
+}
+
+size_t dec_batch_ws(const BatchPlan& bp, DecodeBufs* b, Seg** dsegs, uint32_t** blk_seg,
+                    uint32_t** chunk_seg, uint8_t* base) {
+    Carver c{base};
+    const size_t ns = bp.segs.size();
+    Seg* sg = c.take<Seg>(ns * sizeof(Seg));
+    uint32_t* bm = c.take<uint32_t>((size_t)bp.nb * 4 + 4);
+    uint32_t* cm = c.take<uint32_t>((size_t)bp.nchunks * 4 + 4);
+    DecodeBufs x;
+    x.chunk = bp.chunk;
+    x.nchunks = bp.nchunks;
+    x.offs = c.take<uint64_t>((size_t)bp.nb * 8 + 8);
+    x.status = c.take<int64_t>((size_t)bp.nb * 8 + 8);
+    x.seq = c.take<uint32_t>((size_t)bp.seq_words * 4);
+    x.exits = c.take<int64_t>((size_t)bp.nchunks * 8 + 8);
+    x.cnt = c.take<uint64_t>((size_t)(bp.nchunks + 1) * 8);
+    x.base = c.take<uint64_t>((size_t)(bp.nchunks + 1) * 8);
+    x.idx_err = c.take<int64_t>(ns * 8);
+    x.bad = c.take<long long>(ns * 8);
+    x.scan_tmp_bytes = decode_scan_tmp_bytes(bp.nchunks);
+    x.scan_tmp = c.take<void>(x.scan_tmp_bytes + 8);
+    if (b) *b = x;
+    if (dsegs) *dsegs = sg;
+    if (blk_seg) *blk_seg = bm;
+    if (chunk_seg) *chunk_seg = cm;
+    return c.off;
+}
+
+// Uploads a batch's segment table without blocking the host: the bytes go
+// through a per-thread pinned staging buffer, which is reused only after the
+// event of its previous copy has completed.
+hipError_t upload_table(const void* host, size_t bytes, void* dev, hipStream_t s) {
+    struct Stage {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    thread_local Stage st;
+    if (st.pending && hipEventSynchronize(st.ev) != hipSuccess) return hipErrorUnknown;
+    st.pending = false;
+    if (st.cap < bytes) {
+        if (st.p) (void)hipHostFree(st.p);
+        st.p = nullptr;
+        st.cap = 0;
+        if (hipHostMalloc(&st.p, bytes, hipHostMallocDefault) != hipSuccess) return hipErrorOutOfMemory;
+        st.cap = bytes;
+    }
+    if (!st.ev && hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) != hipSuccess)
+        return hipErrorUnknown;
+    memcpy(st.p, host, bytes);
+    hipError_t e = hipMemcpyAsync(dev, st.p, bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(st.ev, s);
+    st.pending = e == hipSuccess;
+    return e;
+}
+
+// Caller workspace, or a stream-ordered allocation owned by `own`.
+int64_t get_ws(void*& ws, size_t ws_bytes, size_t need, DevBuf& own, hipStream_t s) {
+    if (!ws) {
+        if (own.alloc(need, s) != hipSuccess) return -1;
+        ws = own.p;
+    } else if (ws_bytes < need || ((uintptr_t)ws & 255)) {
+        return kErrUnsupported;
+    }
+    return 0;
+}
+
+}  // namespace
+
+size_t bshuf_compress_lz4_batch_dev_workspace(const size_t* sizes, size_t count, size_t elem_size,
+                                              size_t block_size) {
+    BatchPlan bp;
+    if (make_batch(nullptr, nullptr, sizes, nullptr, count, elem_size, block_size, bp)) return 0;
+    return enc_batch_ws(bp, nullptr, nullptr, nullptr, nullptr);
+}
+
+int64_t bshuf_compress_lz4_batch_dev(const void* const* in, void* const* out, const size_t* sizes,
+                                     size_t count, size_t elem_size, size_t block_size, void* ws,
+                                     size_t ws_bytes, int64_t* d_results, uint64_t* block_offsets,
+                                     void* stream) {
+    BatchPlan bp;
+    const int64_t r = make_batch(in, out, sizes, nullptr, count, elem_size, block_size, bp);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    hipStream_t s = (hipStream_t)stream;
+    for (size_t i = 0; i < count; i++) bp.segs[i].result = d_results + i;
+    // blocks of both LZ4 table types in one batch (a byU32-size block_size
+    // with a byU16-size partial block): one stream at a time
+    const bool wide = (int64_t)bp.L.bs * bp.L.E >= kU16TableLimit;
+    bool mixed = false;
+    for (const Seg& g : bp.segs) mixed = mixed || (g.last && ((int64_t)g.last * bp.L.E >= kU16TableLimit) != wide);
+    if (mixed) {
+        for (size_t i = 0; i < count; i++) {
+            const int64_t e = bshuf_compress_lz4_dev(in[i], out[i], sizes[i], elem_size, block_size,
+                                                     nullptr, 0, d_results + i,
+                                                     block_offsets ? block_offsets + bp.segs[i].first : nullptr,
+                                                     stream);
+            if (e) return e;
+        }
+        return 0;
+    }
+    DevBuf own;
+    const size_t need = enc_batch_ws(bp, nullptr, nullptr, nullptr, nullptr);
+    const int64_t w = get_ws(ws, ws_bytes, need, own, s);
+    if (w) return w;
+    EncodeBufs b;
+    Seg* dsegs = nullptr;
+    uint32_t* blk_seg = nullptr;
+    enc_batch_ws(bp, &b, &dsegs, &blk_seg, (uint8_t*)ws);
+    if (upload_table(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
+        launch_seg_map(dsegs, (int)count, blk_seg, false, s) != hipSuccess ||
+        launch_encode_batch(dsegs, bp.segs.data(), (int)count, blk_seg, bp.L, b, block_offsets, s) !=
+            hipSuccess)
+        return kErrHip;
+    return 0;
+}
+
+size_t bshuf_decompress_lz4_batch_dev_workspace(const size_t* in_nbytes, const size_t* sizes,
+                                                size_t count, size_t elem_size, size_t block_size) {
+    BatchPlan bp;
+    if (make_batch(nullptr, nullptr, sizes, in_nbytes, count, elem_size, block_size, bp)) return 0;
+    return dec_batch_ws(bp, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_nbytes,
+                                       void* const* out, const size_t* sizes, size_t count,
+                                       size_t elem_size, size_t block_size, void* ws,
+                                       size_t ws_bytes, int64_t* d_results, void* stream) {
+    BatchPlan bp;
+    const int64_t r = make_batch(in, out, sizes, in_nbytes, count, elem_size, block_size, bp);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    hipStream_t s = (hipStream_t)stream;
+    for (size_t i = 0; i < count; i++) bp.segs[i].result = d_results + i;
+    DevBuf own;
+    const size_t need = dec_batch_ws(bp, nullptr, nullptr, nullptr, nullptr, nullptr);
+    const int64_t w = get_ws(ws, ws_bytes, need, own, s);
+    if (w) return w;
+    DecodeBufs b;
+    Seg* dsegs = nullptr;
+    uint32_t *blk_seg = nullptr, *chunk_seg = nullptr;
+    dec_batch_ws(bp, &b, &dsegs, &blk_seg, &chunk_seg, (uint8_t*)ws);
+    if (upload_table(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
+        launch_seg_map(dsegs, (int)count, blk_seg, false, s) != hipSuccess ||
+        launch_seg_map(dsegs, (int)count, chunk_seg, true, s) != hipSuccess ||
+        launch_index_batch(dsegs, (int)count, chunk_seg, bp.L, bp.nchunks, b, s) != hipSuccess ||
+        launch_decode_batch(dsegs, bp.segs.data(), (int)count, blk_seg, bp.L, b, s) != hipSuccess)
         return kErrHip;
     return 0;
 }

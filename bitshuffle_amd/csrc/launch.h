@@ -33,6 +33,29 @@ int diag_variant();  // timing ablations (wrong output), diag build only
 // dynamic LDS included) x CUs of the current device, capped by the work.
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work);
 
+// One independent framed stream of a batch (bshuf_*_lz4_batch_dev).  All
+// streams of a batch share elem_size and block_size; global block k of the
+// batch is block k - first of stream blk_seg[k].  The single-stream entry
+// points run without a segment table (segs == nullptr).
+struct Seg {
+    const uint8_t* in;   // encoder: raw input; decoder: framed stream
+    uint8_t* out;        // encoder: framed output; decoder: raw output
+    int64_t first;       // first global block index
+    int64_t nfull;       // full blocks
+    int64_t tail;        // raw tail bytes ((size % 8) * elem_size)
+    int64_t in_nbytes;   // decoder: readable bytes of the framed stream
+    int64_t chunk0;      // decoder: first global index-rebuild chunk
+    int64_t nchunks;     // decoder: index-rebuild chunks of this stream
+    int64_t seq0;        // decoder: first u32 of this stream's token-position area
+    int64_t* result;     // device: bytes written / consumed, or the error code
+    int32_t last;        // elements in the partial block (0 = none)
+    int32_t pad_;
+};
+
+// Fills blk_seg[segs[s].first .. + nblocks(s)) = s for every segment, or with
+// chunks = true chunk_seg[segs[s].chunk0 .. + nchunks) = s.
+hipError_t launch_seg_map(const Seg* segs, int nsegs, uint32_t* map, bool chunks, hipStream_t s);
+
 // Transpose tiles: 256 groups (2048 elements) per 256-thread workgroup.
 constexpr int kTileGroups = 256;
 
@@ -53,6 +76,14 @@ size_t encode_scan_tmp_bytes(int64_t nblocks);
 int64_t encode_slot_bytes(const Layout& L);
 hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64_t tail_bytes,
                          const EncodeBufs& b, int64_t* d_result, hipStream_t s);
+// Batch of independent streams: segs (device) / hsegs (host copy) describe
+// them, L carries the shared bs and E and L.nfull = total blocks.  Every
+// stream's blocks must use one LZ4 table type (bs * E < 65547, or every
+// block at least that long).  block_offsets (optional): per global block, the
+// header offset inside its own stream.
+hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
+                               const Layout& L, const EncodeBufs& b, uint64_t* block_offsets,
+                               hipStream_t s);
 // Largest block (bytes) the LDS-resident encoder/decoder accepts.
 int64_t max_device_block_bytes();
 
@@ -79,6 +110,12 @@ hipError_t launch_index(const uint8_t* in, int64_t blocks_end, const Layout& L,
 hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
                          hipStream_t s);
+// Batch versions: L.nfull = total blocks; b.idx_err and b.bad hold one word
+// per stream; chunk_seg / blk_seg map global chunks / blocks to streams.
+hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_seg, const Layout& L,
+                              int64_t nchunks, const DecodeBufs& b, hipStream_t s);
+hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
+                               const Layout& L, const DecodeBufs& b, hipStream_t s);
 
 // ---- synthetic inputs ----------------------------------------------------
 hipError_t launch_synth(void* out, size_t n, int gen, uint64_t first, uint64_t seed,

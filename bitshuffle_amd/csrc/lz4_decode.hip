@@ -52,13 +52,65 @@ __device__ int64_t chase(const uint8_t* in, int64_t p, int64_t stop, int64_t Cb,
     return p;
 }
 
-__global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in, int64_t Cb,
-                                                  int64_t CH, int64_t W, uint32_t maxlen,
-                                                  int64_t* __restrict__ exits) {
+// Chunk c of the index rebuild: its stream (the single one, or stream
+// chunk_seg[c] of a batch), its chunk number inside that stream and where that
+// stream's blocks and error word live.
+struct IdxArgs {
+    const uint8_t* in;   // single stream
+    int64_t Cb;          // single stream: framed region bytes
+    int64_t nblocks;
+    int64_t* err;
+    const Seg* segs;     // batch (nullptr: single stream)
+    const uint32_t* chunk_seg;
+    int64_t* errs;       // batch: one word per stream
+    int64_t CH;          // chunk bytes
+    int64_t W;           // candidate window (largest record)
+    uint32_t maxlen;
+};
+
+struct ChunkLoc {
+    const uint8_t* in;
+    int64_t Cb;
+    int64_t s;      // chunk index inside the stream
+    int64_t c0;     // global index of the stream's first chunk
+    int64_t first;  // global index of the stream's first block
+    int64_t nb;     // blocks of the stream
+    int64_t* err;
+};
+
+__device__ __forceinline__ ChunkLoc chunk_loc(const IdxArgs& x, int64_t c) {
+    ChunkLoc l;
+    if (!x.segs) {
+        l.in = x.in;
+        l.Cb = x.Cb;
+        l.s = c;
+        l.c0 = 0;
+        l.first = 0;
+        l.nb = x.nblocks;
+        l.err = x.err;
+    } else {
+        const uint32_t g = x.chunk_seg[c];
+        const Seg& sg = x.segs[g];
+        l.in = sg.in;
+        l.Cb = max(sg.in_nbytes - sg.tail, (int64_t)0);
+        l.s = c - sg.chunk0;
+        l.c0 = sg.chunk0;
+        l.first = sg.first;
+        l.nb = sg.nfull + (sg.last ? 1 : 0);
+        l.err = x.errs + g;
+    }
+    return l;
+}
+
+__global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict__ exits) {
     __shared__ __attribute__((aligned(16))) uint8_t win[kIdxWinMax + 64];
     int win_off = 0;
     const int lane = threadIdx.x;
-    const int64_t s = blockIdx.x;
+    const ChunkLoc L = chunk_loc(x, blockIdx.x);
+    const uint8_t* in = L.in;
+    const int64_t Cb = L.Cb, CH = x.CH, W = x.W;
+    const uint32_t maxlen = x.maxlen;
+    const int64_t s = L.s;
     const int64_t cs = s * CH;
     const int64_t ce = min(cs + CH, Cb);
     const int64_t cend = (s == 0) ? cs + 1 : min(cs + W, Cb);  // candidate window
@@ -81,10 +133,10 @@ __global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in
     auto try_cand = [&](int64_t c, uint32_t len) {
         if (c >= cend || c + 4 > Cb) return;
         if (len == 0 || len > maxlen || c + 4 + (int64_t)len > Cb) return;
-        const int64_t x = chase(in, c + 4 + len, ce, Cb, maxlen);
-        if (x == kDead) return;
-        lo = min(lo, x);
-        hi = max(hi, x);
+        const int64_t xx = chase(in, c + 4 + len, ce, Cb, maxlen);
+        if (xx == kDead) return;
+        lo = min(lo, xx);
+        hi = max(hi, xx);
     };
     if (use_lds) {
         // 4 consecutive candidates per lane: two dword reads cover the 7
@@ -107,11 +159,12 @@ __global__ __launch_bounds__(64) void k_idx_exits(const uint8_t* __restrict__ in
         lo = min(lo, (int64_t)__shfl_xor(lo, o));
         hi = max(hi, (int64_t)__shfl_xor(hi, o));
     }
-    if (lane == 0) exits[s] = (hi < 0) ? kDead : (lo == hi ? lo : kAmbiguous);
+    if (lane == 0) exits[blockIdx.x] = (hi < 0) ? kDead : (lo == hi ? lo : kAmbiguous);
 }
 
-// Entry e_s of chunk s: the agreed exit of chunk s-1, else chase forward from
-// the nearest chunk with an agreed exit (or from offset 0).
+// Entry e_s of chunk s (of the stream whose chunk 0 is exits[0]): the agreed
+// exit of chunk s-1, else chase forward from the nearest chunk with an agreed
+// exit (or from offset 0).
 __device__ int64_t chunk_entry(const uint8_t* in, const int64_t* exits, int64_t s, int64_t CH,
                                int64_t Cb, uint32_t maxlen) {
     if (s == 0) return 0;
@@ -122,49 +175,59 @@ __device__ int64_t chunk_entry(const uint8_t* in, const int64_t* exits, int64_t 
     return p;
 }
 
-// Walk chunk s from its entry.  mode 0: count headers into cnt[s];
-// mode 1: write offs[base[s] + i].  Any broken link sets *err.
-__global__ __launch_bounds__(64) void k_idx_walk(const uint8_t* __restrict__ in, int64_t Cb,
-                                                 int64_t CH, uint32_t maxlen,
+// Walk chunk c from its entry.  mode 0: count headers into cnt[c];
+// mode 1: write the offsets of the stream's blocks (base = exclusive scan of
+// the counts over all chunks of all streams).  A broken link sets the
+// stream's error word.
+__global__ __launch_bounds__(64) void k_idx_walk(IdxArgs x, int64_t nchunks_total,
                                                  const int64_t* __restrict__ exits,
                                                  uint64_t* __restrict__ cnt,
                                                  const uint64_t* __restrict__ base,
-                                                 uint64_t* __restrict__ offs, int64_t nblocks,
-                                                 int64_t* __restrict__ err, int mode) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nchunks = (Cb + CH - 1) / CH;
-    if (s >= nchunks) return;
-    const int64_t ce = min((s + 1) * CH, Cb);
-    int64_t p = chunk_entry(in, exits, s, CH, Cb, maxlen);
+                                                 uint64_t* __restrict__ offs, int mode) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks_total) return;
+    const ChunkLoc L = chunk_loc(x, c);
+    const int64_t CH = x.CH, Cb = L.Cb;
+    const uint32_t maxlen = x.maxlen;
+    const int64_t ce = min((L.s + 1) * CH, Cb);
+    int64_t p = chunk_entry(L.in, exits + L.c0, L.s, CH, Cb, maxlen);
     if (p == kDead) {
-        atomicMax((unsigned long long*)err, 1ull);
+        atomicMax((unsigned long long*)L.err, 1ull);
         return;
     }
-    uint64_t k = mode ? base[s] : 0;
-    uint64_t c = 0;
+    uint64_t k = mode ? base[c] - base[L.c0] : 0;  // block index inside the stream
+    uint64_t n = 0;
     while (p < ce) {
         if (p + 4 > Cb) {
-            atomicMax((unsigned long long*)err, 1ull);
+            atomicMax((unsigned long long*)L.err, 1ull);
             return;
         }
-        const uint32_t len = be32_global(in + p);
+        const uint32_t len = be32_global(L.in + p);
         if (len == 0 || len > maxlen || p + 4 + (int64_t)len > Cb) {
-            atomicMax((unsigned long long*)err, 1ull);
+            atomicMax((unsigned long long*)L.err, 1ull);
             return;
         }
         if (mode) {
-            if ((int64_t)k < nblocks) offs[k] = (uint64_t)p;
+            if ((int64_t)k < L.nb) offs[L.first + k] = (uint64_t)p;
             k++;
         }
-        c++;
+        n++;
         p += 4 + len;
     }
-    if (!mode) cnt[s] = c;
+    if (!mode) cnt[c] = n;
 }
 
-__global__ void k_idx_check(const uint64_t* base, int64_t nchunks, int64_t nblocks,
-                            int64_t* err) {
-    if (threadIdx.x == 0 && (int64_t)base[nchunks] != nblocks) atomicMax((unsigned long long*)err, 2ull);
+// Every stream must have produced exactly its number of headers.
+__global__ void k_idx_check(IdxArgs x, const uint64_t* base, int64_t nchunks) {
+    if (!x.segs) {
+        if (threadIdx.x == 0 && (int64_t)base[nchunks] != x.nblocks)
+            atomicMax((unsigned long long*)x.err, 2ull);
+        return;
+    }
+    const Seg& g = x.segs[blockIdx.x];
+    const int64_t nb = g.nfull + (g.last ? 1 : 0);
+    if (threadIdx.x == 0 && (int64_t)(base[g.chunk0 + g.nchunks] - base[g.chunk0]) != nb)
+        atomicMax((unsigned long long*)(x.errs + blockIdx.x), 2ull);
 }
 
 // ---------------------------------------------------------------------------
@@ -336,7 +399,45 @@ struct DecArgs {
     uint32_t maxlen;
     int32_t cap;     // LDS bytes reserved for the decoded block
     uint32_t* seq;   // token positions (k_seq_scan -> lz4_exec_block)
+    const Seg* segs; // batch: per-stream table (nullptr: the single stream above)
+    const uint32_t* blk_seg;
 };
+
+// Where block k lives: its stream's framed bytes, output, token-position area
+// and failure word, its element count and whether it is its stream's last.
+struct BlockLoc {
+    const uint8_t* in;
+    int64_t in_nbytes;
+    uint8_t* out;       // the block's decoded bytes
+    uint32_t* seq;
+    long long* bad;
+    int m;
+    bool last;
+};
+
+__device__ __forceinline__ BlockLoc block_loc(const DecArgs& a, int64_t k, int64_t nb, uint32_t s) {
+    BlockLoc b;
+    if (!a.segs) {
+        b.in = a.in;
+        b.in_nbytes = a.in_nbytes;
+        b.out = a.out + k * (int64_t)a.L.bs * a.L.E;
+        b.seq = a.seq;
+        b.bad = a.bad;
+        b.m = k < a.L.nfull ? a.L.bs : a.L.last;
+        b.last = k + 1 >= nb;
+    } else {
+        const Seg& g = a.segs[s];
+        const int64_t local = k - g.first;
+        b.in = g.in;
+        b.in_nbytes = g.in_nbytes;
+        b.out = g.out + local * (int64_t)a.L.bs * a.L.E;
+        b.seq = a.seq + g.seq0;
+        b.bad = a.bad + s;
+        b.m = local < g.nfull ? a.L.bs : g.last;
+        b.last = local + 1 >= g.nfull + (g.last ? 1 : 0);
+    }
+    return b;
+}
 
 // Record span [o0, o1) clamped into the stream: an offset the index could not
 // resolve (launch_index leaves it at the all-ones sentinel) or a corrupt one
@@ -356,6 +457,7 @@ __device__ __forceinline__ void clamp_span(int64_t& o0, int64_t& o1, int64_t in_
 struct Span {
     int64_t o0, o1;
     int64_t scan;  // k_seq_scan's result: sequence count, or the block's error code
+    BlockLoc loc;
 };
 
 // 16-byte chunks covering a record of an 8 KiB block: (8244 + 30) / 16 / 64 -> 9.
@@ -370,10 +472,10 @@ struct PayRegs {
 // absolute address (a granule never crosses a page: the extra bytes at either
 // end cannot fault and are never used); they land in LDS at Cbuf + (addr & 15).
 __device__ __forceinline__ const gbl128c* span_base(const DecArgs& a, const Span& sp) {
-    return g128_aligned_down(a.in + sp.o0);
+    return g128_aligned_down(sp.loc.in + sp.o0);
 }
 __device__ __forceinline__ int span_shift(const DecArgs& a, const Span& sp) {
-    return (int)((uintptr_t)(a.in + sp.o0) & 15);
+    return (int)((uintptr_t)(sp.loc.in + sp.o0) & 15);
 }
 __device__ __forceinline__ int span_chunks(const DecArgs& a, const Span& sp) {
     return (span_shift(a, sp) + (int)(sp.o1 - sp.o0) + 15) >> 4;
@@ -391,7 +493,7 @@ __device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Sp
         const int c = it * kWave + lane;
         if (c < nch) R.v[it] = g4[c];
     }
-    R.pos = a.seq[sp.o0 / 3 + lane];
+    R.pos = sp.loc.seq[sp.o0 / 3 + lane];
 }
 
 __device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, const Span& sp,
@@ -411,31 +513,34 @@ __device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, con
 // for, right away).
 struct OffRegs {
     uint64_t v;
-    bool last;  // k is the last block: the record end is bounded by maxlen
+    int64_t k;  // block index
 };
 
 __device__ __forceinline__ OffRegs issue_offs(const DecArgs& a, int64_t k, int64_t nb, int lane) {
     OffRegs r;
     r.v = 0;
-    r.last = k + 1 >= nb;
+    r.k = k;
     if (lane < 2) {
         if (k + lane < nb) r.v = a.offs[k + lane];
     } else if (lane == 2) {
         r.v = (uint64_t)a.status[k];  // the scan's verdict
+    } else if (lane == 3 && a.segs) {
+        r.v = a.blk_seg[k];  // the block's stream (batch)
     }
     return r;
 }
 
-__device__ __forceinline__ Span span_from(const DecArgs& a, const OffRegs& r) {
+__device__ __forceinline__ Span span_from(const DecArgs& a, const OffRegs& r, int64_t nb) {
     auto rl = [&](int l) {
         return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(r.v >> 32), l) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)r.v, l));
     };
     Span sp;
+    sp.loc = block_loc(a, r.k, nb, (uint32_t)__builtin_amdgcn_readlane((int)r.v, 3));
     sp.o0 = rl(0);
-    sp.o1 = r.last ? sp.o0 + 4 + (int64_t)a.maxlen : rl(1);
+    sp.o1 = sp.loc.last ? sp.o0 + 4 + (int64_t)a.maxlen : rl(1);
     sp.scan = rl(2);
-    clamp_span(sp.o0, sp.o1, a.in_nbytes, a.maxlen);
+    clamp_span(sp.o0, sp.o1, sp.loc.in_nbytes, a.maxlen);
     return sp;
 }
 
@@ -486,21 +591,21 @@ struct GReader {
 __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= nb) return;
-    const int m = k < a.L.nfull ? a.L.bs : a.L.last;
-    const int n = m * a.L.E;
+    const BlockLoc loc = block_loc(a, k, nb, a.segs ? a.blk_seg[k] : 0u);
+    const int n = loc.m * a.L.E;
     int64_t o0 = (int64_t)a.offs[k];
-    int64_t o1 = (k + 1 < nb) ? (int64_t)a.offs[k + 1] : o0 + 4 + (int64_t)a.maxlen;
-    clamp_span(o0, o1, a.in_nbytes, a.maxlen);
+    int64_t o1 = !loc.last ? (int64_t)a.offs[k + 1] : o0 + 4 + (int64_t)a.maxlen;
+    clamp_span(o0, o1, loc.in_nbytes, a.maxlen);
     const int64_t avail = o1 - o0;
-    const int64_t clen = avail >= 4 ? (int64_t)(int32_t)be32_global(a.in + o0) : 0;
-    int64_t st = header_status(clen, avail, k + 1 == nb, a.maxlen);
+    const int64_t clen = avail >= 4 ? (int64_t)(int32_t)be32_global(loc.in + o0) : 0;
+    int64_t st = header_status(clen, avail, loc.last, a.maxlen);
     if (st == 0) {
         int cnt = 0;
         GReader rd;
         rd.g.w0 = -(1 << 30);
-        rd.P = a.in + o0 + 4;
+        rd.P = loc.in + o0 + 4;
         rd.clen = (int)clen;
-        const int r = scan_block(rd, (int)clen, n, a.seq + o0 / 3, cnt);
+        const int r = scan_block(rd, (int)clen, n, loc.seq + o0 / 3, cnt);
         st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
     }
     a.status[k] = st;
@@ -516,7 +621,7 @@ __device__ __forceinline__ uint32_t land_record(const PayRegs& R, bool in_regs, 
     const gbl128c* g4 = span_base(a, sp);
     const int nch = span_chunks(a, sp);
     for (int c = lane; c < nch; c += kWave) ((lds128*)Cbuf)[c] = g4[c];
-    return a.seq[sp.o0 / 3 + lane];
+    return sp.loc.seq[sp.o0 / 3 + lane];
 }
 
 // Persistent: workgroup w decodes blocks w, w+G, ...  Software pipeline, per
@@ -537,7 +642,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     if (blk >= nb) return;
 
     PayRegs R;
-    Span cur = span_from(a, issue_offs(a, blk, nb, lane));
+    Span cur = span_from(a, issue_offs(a, blk, nb, lane), nb);
     uint32_t cur_pos;
     {
         const bool in_regs = span_fits(a, cur);
@@ -545,21 +650,20 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         cur_pos = land_record(R, in_regs, a, cur, Cbuf, lane);
     }
     int64_t next = blk + stride;
-    Span nxt = {0, 0, 0};
+    Span nxt = {};
     bool nxt_in_regs = false;
     if (next < nb) {
-        nxt = span_from(a, issue_offs(a, next, nb, lane));
+        nxt = span_from(a, issue_offs(a, next, nb, lane), nb);
         nxt_in_regs = span_fits(a, nxt);
         if (nxt_in_regs) issue_pay(R, a, nxt, lane);
     }
-    OffRegs O{0, true};
+    OffRegs O{0, 0};
     if (next + stride < nb) O = issue_offs(a, next + stride, nb, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
     for (;;) {
-        const int m = blk < a.L.nfull ? a.L.bs : a.L.last;
-        const int P = m / 8;
+        const int P = cur.loc.m / 8;
         const int cp = span_shift(a, cur);
         const lds8* C = Cbuf + cp;
         // the scan's verdict: sequence count, or the block's error code
@@ -569,26 +673,26 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         } else {
             clen = (int)(((uint32_t)C[0] << 24) | ((uint32_t)C[1] << 16) | ((uint32_t)C[2] << 8) | C[3]);
             if (!(VAR & 64))
-                lz4_exec_block(Cbuf, cp + 4, D, a.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
+                lz4_exec_block(Cbuf, cp + 4, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // the next record replaces this one in LDS; then the loads two ahead
         const int64_t nn = next + stride;
-        Span nxt2 = {0, 0, 0};
+        Span nxt2 = {};
         bool nxt2_in_regs = false;
         uint32_t nxt_pos = 0;
         if (next < nb) {
             nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
             if (nn < nb) {
-                nxt2 = span_from(a, O);
+                nxt2 = span_from(a, O, nb);
                 if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
                 nxt2_in_regs = span_fits(a, nxt2);
                 if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
             }
         }
         if (status == 0 && !(VAR & 8)) {
-            uint8_t* dst = a.out + blk * (int64_t)a.L.bs * E;
+            uint8_t* dst = cur.loc.out;
             if constexpr (EK != 0) {
                 for (int g = lane; g < P; g += kWave) {
                     uint32_t w[2 * EK];
@@ -616,7 +720,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                 }
             }
         } else if (lane == 0) {
-            atomicMax(a.bad, (long long)blk);
+            atomicMax(cur.loc.bad, (long long)blk);
         }
         if (lane == 0) a.status[blk] = status == 0 ? (int64_t)clen + 4 : (int64_t)status;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -672,28 +776,26 @@ size_t decode_scan_tmp_bytes(int64_t nchunks) {
     return bytes;
 }
 
-hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const DecodeBufs& b,
-                        hipStream_t s) {
-    const int64_t nb = L.nblocks();
-    hipError_t e = hipMemsetAsync(b.idx_err, 0, sizeof(int64_t), s);
+namespace {
+
+// Index rebuild over nch chunks (of one stream, or of every stream of a batch).
+hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, const DecodeBufs& b,
+                      hipStream_t s) {
+    hipError_t e = hipMemsetAsync(b.idx_err, 0, sizeof(int64_t) * (size_t)nsegs, s);
     if (e != hipSuccess || nb == 0) return e;
     // offsets a broken chain never reaches stay at the all-ones sentinel
     // (clamp_span turns them into -1001 without reading the stream)
     e = hipMemsetAsync(b.offs, 0xFF, (size_t)nb * sizeof(uint64_t), s);
-    if (e != hipSuccess) return e;
-    const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
-    const int64_t W = 4 + (int64_t)maxlen;
-    const int64_t nch = b.nchunks;
+    if (e != hipSuccess || nch == 0) return e;
     {
         ProfScope prof("k_idx_exits", s);
-        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), 0, s, in, Cb, b.chunk, W,
-                           maxlen, b.exits);
+        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), 0, s, x, b.exits);
     }
     const unsigned wg = (unsigned)((nch + 63) / 64);
     {
         ProfScope prof("k_idx_walk_count", s);
-        hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, in, Cb, b.chunk, maxlen, b.exits,
-                           b.cnt, (const uint64_t*)nullptr, (uint64_t*)nullptr, nb, b.idx_err, 0);
+        hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, x, nch, b.exits, b.cnt,
+                           (const uint64_t*)nullptr, (uint64_t*)nullptr, 0);
     }
     e = hipMemsetAsync(b.cnt + nch, 0, sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
@@ -705,12 +807,98 @@ hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const De
     if (e != hipSuccess) return e;
     {
         ProfScope prof("k_idx_walk_write", s);
-        hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, in, Cb, b.chunk, maxlen, b.exits,
-                           b.cnt, b.base, b.offs, nb, b.idx_err, 1);
+        hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, x, nch, b.exits, b.cnt, b.base,
+                           b.offs, 1);
     }
-    hipLaunchKernelGGL(k_idx_check, dim3(1), dim3(64), 0, s, b.base, nch, nb, b.idx_err);
+    hipLaunchKernelGGL(k_idx_check, dim3((unsigned)(x.segs ? nsegs : 1)), dim3(64), 0, s, x, b.base,
+                       nch);
     return hipGetLastError();
 }
+
+}  // namespace
+
+hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const DecodeBufs& b,
+                        hipStream_t s) {
+    const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
+    IdxArgs x{in, Cb, L.nblocks(), b.idx_err, nullptr, nullptr, nullptr, b.chunk,
+              4 + (int64_t)maxlen, maxlen};
+    return index_impl(x, L.nblocks(), b.nchunks, 1, b, s);
+}
+
+hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_seg, const Layout& L,
+                              int64_t nchunks, const DecodeBufs& b, hipStream_t s) {
+    const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
+    IdxArgs x{nullptr, 0, L.nfull, nullptr, segs, chunk_seg, b.idx_err, b.chunk,
+              4 + (int64_t)maxlen, maxlen};
+    return index_impl(x, L.nfull, nchunks, nsegs, b, s);
+}
+
+namespace {
+
+// Scan + decode kernels over nb blocks (one stream, or all streams of a batch).
+hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
+    const Layout& L = a.L;
+    // decoded block + record (header, payload, 16-byte alignment slack)
+    const size_t rec = (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
+    const size_t lds = (size_t)a.cap + 16 + rec;
+    const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
+    const void* fn = nullptr;
+#define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
+    switch (ek) {
+        case 1: fn = BSHUF_DEC(1, 0); break;
+        case 2:
+            fn = BSHUF_DEC(2, 0);
+#ifdef BSHUF_DIAG
+            // diagnostic build only -- ABLATIONS for timing, wrong output:
+            // 8 no output stores, 64 no sequence execution
+            if (diag_variant() == 8) fn = BSHUF_DEC(2, 8);
+            if (diag_variant() == 64) fn = BSHUF_DEC(2, 64);
+            if (diag_variant() == 72) fn = BSHUF_DEC(2, 72);
+#endif
+            break;
+        case 4: fn = BSHUF_DEC(4, 0); break;
+        case 8: fn = BSHUF_DEC(8, 0); break;
+        default: fn = BSHUF_DEC(0, 0); break;
+    }
+#undef BSHUF_DEC
+    hipError_t e;
+    {
+        ProfScope prof("k_seq_scan", s);
+        hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, a, nb);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (lds > 65536) {
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    const dim3 grid((unsigned)persistent_grid(fn, kWave, lds, nb));
+    ProfScope prof("k_lz4_decode", s);
+    void* args[] = {&a, const_cast<int64_t*>(&nb)};
+    e = hipLaunchKernel(fn, grid, dim3(kWave), args, lds, s);
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+// Batch result per stream: bytes consumed, or the error of its LAST failing
+// block (one workgroup per stream; same rules as k_decode_finish).
+__global__ __launch_bounds__(64) void k_decode_finish_batch(const int64_t* __restrict__ status,
+                                                            const uint64_t* __restrict__ offs,
+                                                            const long long* bad,
+                                                            const int64_t* idx_err, const Seg* segs,
+                                                            int32_t bs, int32_t E) {
+    const Seg& g = segs[blockIdx.x];
+    const int64_t nb = g.nfull + (g.last ? 1 : 0);
+    const long long last_bad = bad[blockIdx.x];
+    const int64_t end = nb ? (int64_t)offs[g.first + nb - 1] + status[g.first + nb - 1] : 0;
+    const bool ok = last_bad < 0 && idx_err[blockIdx.x] == 0 && end + g.tail <= g.in_nbytes;
+    uint8_t* tail_dst = g.out + (g.nfull * (int64_t)bs + g.last) * E;
+    if (ok)
+        for (int64_t i = threadIdx.x; i < g.tail; i += blockDim.x) tail_dst[i] = g.in[end + i];
+    if (threadIdx.x == 0) *g.result = last_bad >= 0 ? status[last_bad] : (!ok ? -91 : end + g.tail);
+}
+
+}  // namespace
 
 hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
@@ -721,48 +909,8 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15), nullptr};
-        // decoded block + record (header, payload, 16-byte alignment slack)
-        const size_t rec = (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
-        const size_t lds = (size_t)a.cap + 16 + rec;
-        const bool aligned = ((uintptr_t)out & 15) == 0;
-        const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
-        a.seq = b.seq;
-        const void* fn = nullptr;
-#define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
-        switch (ek) {
-            case 1: fn = BSHUF_DEC(1, 0); break;
-            case 2:
-                fn = BSHUF_DEC(2, 0);
-#ifdef BSHUF_DIAG
-                // diagnostic build only -- ABLATIONS for timing, wrong output:
-                // 8 no output stores, 64 no sequence execution
-                if (diag_variant() == 8) fn = BSHUF_DEC(2, 8);
-                if (diag_variant() == 64) fn = BSHUF_DEC(2, 64);
-                if (diag_variant() == 72) fn = BSHUF_DEC(2, 72);
-#endif
-                break;
-            case 4: fn = BSHUF_DEC(4, 0); break;
-            case 8: fn = BSHUF_DEC(8, 0); break;
-            default: fn = BSHUF_DEC(0, 0); break;
-        }
-#undef BSHUF_DEC
-        {
-            ProfScope prof("k_seq_scan", s);
-            hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, a, nb);
-            e = hipGetLastError();
-            if (e != hipSuccess) return e;
-        }
-        if (lds > 65536) {
-            e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
-        const dim3 grid((unsigned)persistent_grid(fn, kWave, lds, nb));
-        ProfScope prof("k_lz4_decode", s);
-        void* args[] = {&a, const_cast<int64_t*>(&nb)};
-        e = hipLaunchKernel(fn, grid, dim3(kWave), args, lds, s);
-        if (e != hipSuccess) return e;
-        e = hipGetLastError();
+                  (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr};
+        e = decode_impl(a, nb, ((uintptr_t)out & 15) == 0, s);
         if (e != hipSuccess) return e;
     }
     uint8_t* tail_dst = out + (L.nfull * (int64_t)L.bs + L.last) * L.E;
@@ -770,6 +918,26 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
     hipLaunchKernelGGL(k_decode_finish, dim3(1), dim3(64), 0, s, b.status, b.offs, nb,
                        (const long long*)b.bad, (const int64_t*)b.idx_err, in, in_nbytes,
                        tail_dst, tail_bytes, d_result);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
+                               const Layout& L, const DecodeBufs& b, hipStream_t s) {
+    const int64_t nb = L.nfull;
+    hipError_t e = hipMemsetAsync(b.bad, 0xFF, sizeof(long long) * (size_t)nsegs, s);
+    if (e != hipSuccess) return e;
+    if (nb > 0) {
+        const int64_t nmax = (int64_t)L.bs * L.E;
+        DecArgs a{nullptr, 0, b.offs, nullptr, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
+                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg};
+        bool aligned = true;
+        for (int i = 0; i < nsegs; i++) aligned = aligned && ((uintptr_t)hsegs[i].out & 15) == 0;
+        e = decode_impl(a, nb, aligned, s);
+        if (e != hipSuccess) return e;
+    }
+    ProfScope prof("k_decode_finish", s);
+    hipLaunchKernelGGL(k_decode_finish_batch, dim3((unsigned)nsegs), dim3(64), 0, s, b.status, b.offs,
+                       (const long long*)b.bad, (const int64_t*)b.idx_err, segs, L.bs, L.E);
     return hipGetLastError();
 }
 

@@ -79,6 +79,8 @@ struct EncArgs {
     Layout L;
     int32_t desc_ok;   // LDS holds kDescBytes of sequence descriptors at D + desc_off
     int32_t desc_off;
+    const Seg* segs;   // batch: per-stream table (nullptr: the single stream in/L)
+    const uint32_t* blk_seg;
 };
 
 // Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
@@ -682,8 +684,18 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     const int64_t stride = gridDim.x;
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
-    auto blk_m = [&](int64_t k) { return k < a.L.nfull ? a.L.bs : a.L.last; };
-    auto blk_src = [&](int64_t k) { return a.in + k * (int64_t)a.L.bs * E; };
+    // block k -> (elements, source): one stream, or a batch of streams
+    constexpr bool kBatch = (VAR & 256) != 0;
+    auto blk_m = [&](int64_t k) {
+        if (!kBatch) return k < a.L.nfull ? a.L.bs : a.L.last;
+        const Seg& g = a.segs[a.blk_seg[k]];
+        return k - g.first < g.nfull ? a.L.bs : g.last;
+    };
+    auto blk_src = [&](int64_t k) {
+        if (!kBatch) return a.in + k * (int64_t)a.L.bs * E;
+        const Seg& g = a.segs[a.blk_seg[k]];
+        return g.in + (k - g.first) * (int64_t)a.L.bs * E;
+    };
 
     BlockRegs<EK> R;
     BlockRegs4<EK> R4;
@@ -807,10 +819,18 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 // record use byte stores (they share dwords with the neighbouring records).
 __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scratch, int64_t slot,
                                                  const uint64_t* __restrict__ offs,
-                                                 uint8_t* __restrict__ out) {
+                                                 uint8_t* __restrict__ out, const Seg* segs,
+                                                 const uint32_t* __restrict__ blk_seg,
+                                                 uint64_t* __restrict__ block_offsets) {
     const int64_t blk = blockIdx.x;
-    const uint64_t rel0 = offs[blk];
+    uint64_t rel0 = offs[blk];
     const int64_t len = (int64_t)(offs[blk + 1] - rel0);
+    if (segs) {  // batch: offsets are relative to the block's own stream
+        const Seg& g = segs[blk_seg[blk]];
+        rel0 -= offs[g.first];
+        out = g.out;
+    }
+    if (block_offsets && threadIdx.x == 0) block_offsets[blk] = rel0;
     const uint8_t* rec = scratch + blk * slot;
     const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(rec);
     // 16-byte chunks of the ABSOLUTE destination address space
@@ -846,6 +866,16 @@ __global__ void k_encode_finish(const uint64_t* offs, int64_t nblocks, const uin
     const uint64_t end = offs[nblocks];
     for (int i = threadIdx.x; i < tail; i += blockDim.x) out[end + i] = tail_src[i];
     if (threadIdx.x == 0) *result = (int64_t)end + tail;
+}
+
+// Batch: one workgroup per stream.
+__global__ void k_encode_finish_batch(const uint64_t* offs, const Seg* segs, int32_t bs, int32_t E) {
+    const Seg& g = segs[blockIdx.x];
+    const int64_t nb = g.nfull + (g.last ? 1 : 0);
+    const uint64_t end = offs[g.first + nb] - offs[g.first];
+    const uint8_t* tail_src = g.in + (g.nfull * (int64_t)bs + g.last) * E;
+    for (int i = threadIdx.x; i < g.tail; i += blockDim.x) g.out[end + i] = tail_src[i];
+    if (threadIdx.x == 0) *g.result = (int64_t)end + g.tail;
 }
 
 // Device check of the property Table::exchange relies on: same-address lanes
@@ -978,7 +1008,7 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
         // table's LDS as staging (every block of up to ~16 KiB)
         const bool desc = !wide && 4 + lz4_bound((int)nmax) + 15 <= kTableBytes;
         const int32_t desc_off = (int32_t)(((nmax + 15) & ~15) + kDataPad);
-        EncArgs a{in, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off};
+        EncArgs a{in, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off, nullptr, nullptr};
         const size_t lds = kTableBytes + (size_t)desc_off + (desc ? kDescBytes : 0);
         // the partial block decides its own table type, so a stream whose full
         // blocks need byU32 but partial block byU16 launches twice
@@ -1028,7 +1058,8 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
     if (nb > 0) {
         ProfScope prof("k_compact", s);
         hipLaunchKernelGGL(k_compact, dim3((unsigned)nb), dim3(256), 0, s, b.scratch, b.slot,
-                           b.offs, out);
+                           b.offs, out, (const Seg*)nullptr, (const uint32_t*)nullptr,
+                           (uint64_t*)nullptr);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1036,6 +1067,76 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
     ProfScope prof("k_encode_finish", s);
     hipLaunchKernelGGL(k_encode_finish, dim3(1), dim3(64), 0, s, b.offs, nb, tail_src, tail_bytes,
                        out, d_result);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
+                               const Layout& L, const EncodeBufs& b, uint64_t* block_offsets,
+                               hipStream_t s) {
+    const int64_t nb = L.nfull;  // total blocks of the batch
+    hipError_t e;
+    if (nb > 0) {
+        const int64_t nmax = (int64_t)L.bs * L.E;
+        const bool wide = nmax >= kU16TableLimit;
+        for (int i = 0; i < nsegs; i++)
+            if (hsegs[i].last && ((int64_t)hsegs[i].last * L.E >= kU16TableLimit) != wide)
+                return hipErrorInvalidValue;  // mixed table types: the caller splits the batch
+        const bool desc = !wide && 4 + lz4_bound((int)nmax) + 15 <= kTableBytes;
+        const int32_t desc_off = (int32_t)(((nmax + 15) & ~15) + kDataPad);
+        EncArgs a{nullptr, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off, segs, blk_seg};
+        const size_t lds = kTableBytes + (size_t)desc_off + (desc ? kDescBytes : 0);
+        bool aligned = true;
+        for (int i = 0; i < nsegs; i++) aligned = aligned && ((uintptr_t)hsegs[i].in & 15) == 0;
+        const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
+#define BSHUF_E(EKV)                                                                  \
+    case EKV:                                                                         \
+        e = wide ? launch_enc_t<EKV, true, 256>(a, nb, lds, s)                        \
+                 : launch_enc_t<EKV, false, 256>(a, nb, lds, s);                      \
+        break;
+        switch (ek) {
+            BSHUF_E(0)
+            BSHUF_E(1)
+            BSHUF_E(2)
+            BSHUF_E(4)
+            BSHUF_E(8)
+            default: e = hipErrorInvalidValue;
+        }
+#undef BSHUF_E
+        if (e != hipSuccess) return e;
+    }
+    e = hipMemsetAsync(b.foot + nb, 0, sizeof(uint64_t), s);
+    if (e != hipSuccess) return e;
+    size_t tmp = b.scan_tmp_bytes;
+    {
+        ProfScope prof("scan_block_offsets", s);
+        e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.foot, b.offs, (int)(nb + 1), s);
+    }
+    if (e != hipSuccess) return e;
+    if (nb > 0) {
+        ProfScope prof("k_compact", s);
+        hipLaunchKernelGGL(k_compact, dim3((unsigned)nb), dim3(256), 0, s, b.scratch, b.slot, b.offs,
+                           (uint8_t*)nullptr, segs, blk_seg, block_offsets);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    ProfScope prof("k_encode_finish", s);
+    hipLaunchKernelGGL(k_encode_finish_batch, dim3((unsigned)nsegs), dim3(64), 0, s, b.offs, segs,
+                       L.bs, L.E);
+    return hipGetLastError();
+}
+
+// map[first .. first + count) = s, one workgroup per segment (blocks or
+// index-rebuild chunks).
+__global__ void k_seg_map(const Seg* segs, uint32_t* map, int chunks) {
+    const Seg& g = segs[blockIdx.x];
+    const int64_t first = chunks ? g.chunk0 : g.first;
+    const int64_t count = chunks ? g.nchunks : g.nfull + (g.last ? 1 : 0);
+    for (int64_t i = threadIdx.x; i < count; i += blockDim.x) map[first + i] = blockIdx.x;
+}
+
+hipError_t launch_seg_map(const Seg* segs, int nsegs, uint32_t* map, bool chunks, hipStream_t s) {
+    if (nsegs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_map, dim3((unsigned)nsegs), dim3(256), 0, s, segs, map, chunks ? 1 : 0);
     return hipGetLastError();
 }
 

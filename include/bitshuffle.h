@@ -63,6 +63,33 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
                                  size_t ws_bytes, int64_t* d_result,
                                  const uint64_t* block_offsets, void* stream);
 
+/* ---- batched device entry points (additive) ----
+ *
+ * `count` independent framed streams per call, all with the same elem_size and
+ * block_size, each with its own (device) input, output and size; one launch
+ * of each kernel covers every block of every stream (the OpenMP block loop of
+ * src/bitshuffle_core.c:1899-1907, widened to many buffers).  in[], out[],
+ * sizes[] and in_nbytes[] are HOST arrays of device pointers / sizes;
+ * d_results is a DEVICE array of `count` int64: per stream, bytes written
+ * (compress) or consumed (decompress), or that stream's negative error code.
+ * A corrupt stream never affects the others.  block_offsets (optional,
+ * device, one u64 per block of the batch in stream order): each block's
+ * header offset inside its own stream.  The per-stream table travels through a
+ * per-thread pinned buffer; nothing synchronises the host.
+ */
+size_t bshuf_compress_lz4_batch_dev_workspace(const size_t* sizes, size_t count, size_t elem_size,
+                                              size_t block_size);
+int64_t bshuf_compress_lz4_batch_dev(const void* const* in, void* const* out, const size_t* sizes,
+                                     size_t count, size_t elem_size, size_t block_size, void* ws,
+                                     size_t ws_bytes, int64_t* d_results, uint64_t* block_offsets,
+                                     void* stream);
+size_t bshuf_decompress_lz4_batch_dev_workspace(const size_t* in_nbytes, const size_t* sizes,
+                                                size_t count, size_t elem_size, size_t block_size);
+int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_nbytes,
+                                       void* const* out, const size_t* sizes, size_t count,
+                                       size_t elem_size, size_t block_size, void* ws,
+                                       size_t ws_bytes, int64_t* d_results, void* stream);
+
 /* Synthetic benchmark inputs of SURVEY.md 8(d), generated on the device
  * (counter based, identical to the CPU definition): gen 0 = int32 ramp,
  * 1 = int16 correlated noise (G1), 2 = float32 smooth field (G2). */

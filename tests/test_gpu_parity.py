@@ -411,3 +411,84 @@ def test_device_api_unaligned_pointers(bs, oracle, torch):
         torch.cuda.synchronize()
         assert r == nbytes
         assert sh[off_out:off_out + nbytes].cpu().numpy().tobytes() == oracle.bitshuffle(a).tobytes()
+
+
+# ------------------------------------------------------------------ batch API
+def test_batch_api_matches_oracle(bs, oracle, torch):
+    """bshuf_*_lz4_batch_dev: streams of different lengths (partial blocks,
+    raw tails, an empty one, one smaller than a block) in ONE launch each way;
+    every stream equals the oracle's own stream, the per-block offsets equal a
+    header walk of each stream, and the decode restores every input."""
+    rng = np.random.default_rng(4)
+    sizes = [3 * 4096 + 1005, 0, 17, 4096, 9 * 4096 + 13, 5000, 123457]
+    arrs = []
+    for i, n in enumerate(sizes):
+        if i % 2:
+            arrs.append(oracle.gen_g1(n, 1000 * i, 12345 + i))
+        else:
+            arrs.append((rng.integers(-2, 3, n).cumsum() % 97).astype(np.int16))
+    for block in (0, 64, 2048):
+        xs = [torch.from_numpy(a.copy()).cuda() for a in arrs]
+        nblk = sum(int(bs.lib.bshuf_lz4_dev_nblocks(a.size, 2, block)) for a in arrs)
+        offs = torch.zeros(max(nblk, 1), dtype=torch.int64, device="cuda")
+        outs = bs.compress_lz4_batch_dev(xs, block, offsets=offs)
+        k = 0
+        host_offs = offs.cpu().numpy()
+        for a, o in zip(arrs, outs):
+            want = oracle.compress_lz4(a, block)
+            got = o.cpu().numpy()
+            assert got.tobytes() == want.tobytes(), (a.size, block)
+            nb = int(bs.lib.bshuf_lz4_dev_nblocks(a.size, 2, block))
+            pos = 0
+            for j in range(nb):
+                assert host_offs[k + j] == pos, (a.size, block, j)
+                pos += 4 + int.from_bytes(want[pos:pos + 4].tobytes(), "big")
+            k += nb
+        dec = bs.decompress_lz4_batch_dev([o.clone() for o in outs], [a.shape for a in arrs],
+                                          torch.int16, block)
+        for a, d in zip(arrs, dec):
+            assert d.cpu().numpy().tobytes() == a.tobytes(), (a.size, block)
+
+
+def test_batch_api_isolates_corrupt_stream(bs, oracle, torch):
+    """A corrupted stream in a batch fails alone, with the single-stream
+    decoder's error code; its neighbours decode correctly."""
+    arrs = [oracle.gen_g1(6 * 4096 + 77, 0, 12345 + i) for i in range(5)]
+    encs = [oracle.compress_lz4(a) for a in arrs]
+    bad = encs[2].copy()
+    bad[4 + 40] ^= 0x5A  # inside block 0's payload
+    bad[-30:] = 0        # and the tail end
+    bufs = [torch.from_numpy(e.copy()).cuda() for e in encs]
+    bufs[2] = torch.from_numpy(bad).cuda()
+    outs, res = bs.decompress_lz4_batch_dev(bufs, [a.shape for a in arrs], torch.int16, sync=False)
+    res = res.cpu().tolist()
+    with pytest.raises(RuntimeError) as single:
+        bs.decompress_lz4_dev(bufs[2], arrs[2].shape, torch.int16)
+    assert res[2] < 0 and res[2] == single.value.args[1]
+    for i in (0, 1, 3, 4):
+        assert res[i] == encs[i].size
+        assert outs[i].cpu().numpy().tobytes() == arrs[i].tobytes()
+
+
+@pytest.mark.slow
+def test_batch_config4_digests(bs, torch):
+    """BASELINE config 4: 32 MiB G1 chunks (seed 12345 + chunk id) compressed
+    as ONE batch equal the reference's digests (chunks 0-3, 511, 1023), and
+    the batch decoder restores them."""
+    full = {e["name"]: e for e in load_vectors()["full"]}
+    names = ["cfg4_g1_chunk%04d" % c for c in (0, 1, 2, 3, 511, 1023)]
+    xs = []
+    for name in names:
+        e = full[name]
+        x = torch.empty(e["size"], dtype=torch.int16, device="cuda")
+        bs.synth_fill_dev(x, 1, seed=e["seed"])
+        xs.append(x)
+    outs = bs.compress_lz4_batch_dev(xs)
+    import hashlib
+    for name, o in zip(names, outs):
+        e = full[name]
+        assert o.numel() == e["compressed_len"], name
+        assert hashlib.sha256(o.cpu().numpy().tobytes()).hexdigest() == e["compressed_sha256"], name
+    dec = bs.decompress_lz4_batch_dev(outs, [x.shape for x in xs], torch.int16)
+    for x, d in zip(xs, dec):
+        assert torch.equal(x, d)
