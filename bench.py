@@ -3,17 +3,27 @@
 encode+decode round trip of 4 GiB int16 (G1 correlated noise, default 8 KiB
 blocks) on MI355X, as GiB/s and as a fraction of the HBM roofline.
 
-One step = bshuf_compress_lz4_dev of the whole 4 GiB buffer (fused transpose +
-LZ4 kernel, offset scan, compaction) + bshuf_decompress_lz4_dev of the framed
-stream it produced (parallel block-index rebuild from the framing -- the
-encoder's offsets are NOT reused -- then fused LZ4 decode + inverse transpose).
-Inputs are generated on the device before timing; nothing crosses PCIe inside
-the timed region except the 8-byte compressed length the decoder needs.
+One step (config 2, the default) = bshuf_compress_lz4_dev of the whole 4 GiB
+buffer (fused transpose + LZ4 kernel, offset scan, compaction) +
+bshuf_decompress_lz4_dev of the framed stream it produced (parallel
+block-index rebuild from the framing -- the encoder's offsets are NOT reused --
+then fused LZ4 decode + inverse transpose).  Inputs are generated on the
+device before timing; nothing crosses PCIe inside the timed region except the
+8-byte compressed length the decoder needs.
 
-Multi-GPU (launched by torch.distributed.run): every rank round-trips its own
-4 GiB shard (seed 12345 + rank) -- blocks and shards are independent, so there
-is no data-path collective; RCCL is used only for the barrier and the max of
-the per-rank times.  value = total uncompressed bytes of all ranks / max time.
+The other BASELINE configs (parity-tested separately, not the headline line):
+  --config 1  bshuf_bitshuffle + bshuf_bitunshuffle of the 64 MiB int32 ramp
+  --config 3  the round trip on 16 GiB float32 G2 (elem_size 4, auto blocks)
+  --config 4  the round trip of 128 independent 32 MiB int16 G1 chunks per
+              GPU (seed 12345 + global chunk id) through the batched API
+              (one launch per kernel for all 128 streams)
+
+Multi-GPU: `--gpus N` without a torch.distributed environment re-launches
+itself under torch.distributed.run with N ranks (before touching the GPU);
+each rank round-trips its own shard (seed 12345 + rank, or its own 128 chunks
+in config 4) -- blocks and shards are independent, so there is no data-path
+collective; RCCL carries only the barrier, the max of the per-rank times and
+the sum of bytes.  value = total uncompressed bytes of all ranks / max time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -21,6 +31,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,25 +43,53 @@ METRIC = "device-resident GiB/s bitshuffle+LZ4 encode+decode, 4 GiB int16; % HBM
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
 
+CONFIGS = {
+    1: dict(gen=0, dtype="int32", gib=1.0 / 16, what="shuffle"),
+    2: dict(gen=1, dtype="int16", gib=4.0, what="lz4"),
+    3: dict(gen=2, dtype="float32", gib=16.0, what="lz4"),
+    4: dict(gen=1, dtype="int16", gib=4.0, what="batch", chunk_mib=32, chunks=128),
+}
+
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--gib", type=float, default=4.0, help="uncompressed GiB per GPU")
-    ap.add_argument("--cpu-sample-mib", type=int, default=512)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--gib", type=float, default=None, help="uncompressed GiB per GPU (override)")
+    ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip per-kernel event timing")
     return ap.parse_args(argv)
 
 
 # ----------------------------------------------------------------- dist utils
+def maybe_spawn(args, argv):
+    """`--gpus N` with N > 1 outside torch.distributed: start N ranks under
+    torch.distributed.run as a CHILD process (nothing has touched the GPU yet)
+    and exit with its status."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def dist_setup(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     if world > 1:
         import torch.distributed as dist
         backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -67,24 +107,24 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(x, world, device):
+def reduce_over_ranks(x, world, device, op):
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def max_over_ranks(x, world, device):
+    import torch.distributed as dist
+    return reduce_over_ranks(x, world, device, dist.ReduceOp.MAX) if world > 1 else x
 
 
 def sum_over_ranks(x, world, device):
-    if world == 1:
-        return x
-    import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return reduce_over_ranks(x, world, device, dist.ReduceOp.SUM) if world > 1 else x
 
 
 def timed_loop(step, steps, warmup, world, sync, device):
@@ -129,47 +169,99 @@ def load_pmc_traffic():
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(sample_mib):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _omp_threads(n):
+    """Thread count of the reference's OpenMP team (libgomp is already loaded
+    by oracle/_ref/libbshuf_ref.so; omp_set_num_threads acts on that copy)."""
+    try:
+        ctypes.CDLL("libgomp.so.1").omp_set_num_threads(int(n))
+        return True
+    except OSError:
+        return False
+
+
+def cpu_baseline(sample_mib, cfg):
     """The reference's own C (oracle/_ref: AVX2 + OpenMP build from the
-    reference sources) timed on this host, on a bounded sample of the same
-    workload.  Falls back to our scalar CPU port when _ref is absent."""
+    reference sources by oracle/Makefile) timed on this host on a bounded
+    sample of the same workload, with 1 thread and with every core of this
+    process's affinity set.  Falls back to our scalar CPU port (1 thread)
+    when _ref is absent."""
     import numpy as np
     from oracle import Oracle, Reference, reference_available
     o = Oracle()
-    n = sample_mib * (1 << 20) // 2
-    a = o.gen_g1(n, 0, 12345)
+    gen = cfg["gen"]
+    es = {0: 4, 1: 2, 2: 4}[gen]
+    n = sample_mib * (1 << 20) // es
+    a = o.gen_g1(n, 0, 12345) if gen == 1 else (o.gen_g2(n, 0, 12345) if gen == 2 else o.gen_g0(n))
+    affinity = len(os.sched_getaffinity(0))
+    # the box's CPU share: OMP_NUM_THREADS when the environment sets it (the
+    # affinity mask may list far more cores than the job may use; 256 OpenMP
+    # threads on a 16-core share run ~25x slower than 16)
+    share = int(os.environ.get("OMP_NUM_THREADS") or affinity)
     if reference_available():
         codec, kind = Reference(), "reference"
-        cores = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count())))
     else:
-        codec, kind, cores = o, "port", 1
-        a = a[: min(n, 1 << 24)]
-    best = None
-    t_all = time.perf_counter()
-    reps = 0
-    while reps < 3 or (time.perf_counter() - t_all < 8.0 and reps < 50):
-        t0 = time.perf_counter()
-        c = codec.compress_lz4(a)
-        t1 = time.perf_counter()
-        d = codec.decompress_lz4(c, a.shape, a.dtype)
-        t2 = time.perf_counter()
-        if reps == 0:
-            assert np.array_equal(d, a)
-        v = a.nbytes / (t2 - t0) / GIB
-        best = v if best is None else max(best, v)
-        reps += 1
-    return {"value": round(best, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
-            "sample": "%d MiB int16 G1 (seed 12345), bitshuffle+LZ4 compress + decompress "
-                      "round trip through the C-ABI, best of %d reps; %s" % (
-                          a.nbytes >> 20, reps,
-                          "reference C from /root/reference compiled -O3 -march=haswell "
-                          "-fopenmp (setup.py flags)" if kind == "reference"
-                          else "scalar oracle port, 1 thread")}
+        codec, kind = o, "port"
+
+    def rate(arr, budget_s):
+        best, reps, t_all = None, 0, time.perf_counter()
+        while reps < 2 or (time.perf_counter() - t_all < budget_s and reps < 20):
+            t0 = time.perf_counter()
+            if cfg["what"] == "shuffle":
+                s = codec.bitshuffle(arr)
+                t1 = time.perf_counter()
+                d = codec.bitunshuffle(s)
+            else:
+                c = codec.compress_lz4(arr)
+                t1 = time.perf_counter()
+                d = codec.decompress_lz4(c, arr.shape, arr.dtype)
+            t2 = time.perf_counter()
+            if reps == 0:
+                assert np.array_equal(d, arr)
+            v = arr.nbytes / (t2 - t0) / GIB
+            best = v if best is None else max(best, v)
+            reps += 1
+        return best, reps
+
+    res = {"unit": "GiB/s", "kind": kind, "cpu_model": cpu_model(), "affinity_cores": affinity,
+           "os_cpu_count": os.cpu_count()}
+    if kind == "reference":
+        _omp_threads(share)
+        v_all, reps_all = rate(a, 8.0)
+        one = a[: max(len(a) // 8, 1 << 16)]
+        _omp_threads(1)
+        v_one, reps_one = rate(one, 6.0)
+        _omp_threads(share)
+        res.update(value=round(v_all, 3), cores=share, value_1thread=round(v_one, 3),
+                   sample="%d MiB %s (seed 12345) on the job's CPU share (OMP_NUM_THREADS), best of %d; %d MiB 1-thread, best "
+                          "of %d; %s round trip through the reference C-ABI, compiled from "
+                          "/root/reference -O3 -march=haswell -fopenmp (setup.py flags)" % (
+                              a.nbytes >> 20, cfg["dtype"], reps_all, one.nbytes >> 20, reps_one,
+                              "bitshuffle+bitunshuffle" if cfg["what"] == "shuffle"
+                              else "bitshuffle+LZ4 compress + decompress"))
+    else:
+        one = a[: min(len(a), 1 << 24)]
+        v_one, reps_one = rate(one, 8.0)
+        res.update(value=round(v_one, 3), cores=1, value_1thread=round(v_one, 3),
+                   sample="%d MiB, scalar oracle port, 1 thread, best of %d" % (
+                       one.nbytes >> 20, reps_one))
+    return res
 
 
 # ----------------------------------------------------------------------- main
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
+    maybe_spawn(args, argv)
     import torch
     world, rank, local = dist_setup(args)
     import bitshuffle_amd as B
@@ -177,34 +269,89 @@ def main(argv=None):
 
     if not B.using_HIP() or not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (MI355X)")
+    cfg = CONFIGS[args.config]
+    gib = args.gib if args.gib is not None else cfg["gib"]
     dev = torch.device("cuda", local)
-    nbytes = int(args.gib * GIB) // 16 * 16
-    n = nbytes // 2
-    x = torch.empty(n, dtype=torch.int16, device=dev)
-    B.synth_fill_dev(x, 1, first=0, seed=12345 + rank)
-    bound = B.compress_lz4_bound(n, 2, 0)
-    comp = torch.empty(bound, dtype=torch.uint8, device=dev)
-    ws_enc = api.compress_lz4_workspace(n, 2, 0, device=dev)
-    ws_dec = api.decompress_lz4_workspace(bound, n, 2, 0, device=dev)
-    res_e = torch.empty(1, dtype=torch.int64, device=dev)
-    res_d = torch.empty(1, dtype=torch.int64, device=dev)
-    y = torch.empty_like(x)
-    clen = [0]
+    dt = {"int16": torch.int16, "int32": torch.int32, "float32": torch.float32}[cfg["dtype"]]
+    es = torch.empty(0, dtype=dt).element_size()
+    lib = B.lib
 
-    def step():
-        api.compress_lz4_dev(x, out=comp, workspace=ws_enc, result=res_e, sync=False)
-        c = int(res_e.item())  # the decoder needs the stream length on the host
-        clen[0] = c
-        api.decompress_lz4_dev(comp[:c], x.shape, x.dtype, out=y, workspace=ws_dec, result=res_d,
-                               sync=False)
+    if cfg["what"] == "batch":
+        cn = cfg["chunk_mib"] * (1 << 20) // es
+        nchunks = max(1, int(gib * GIB) // (cfg["chunk_mib"] << 20))
+        xs = [torch.empty(cn, dtype=dt, device=dev) for _ in range(nchunks)]
+        for i, x in enumerate(xs):
+            B.synth_fill_dev(x, cfg["gen"], seed=12345 + rank * nchunks + i)
+        nbytes = cn * es * nchunks
+        outs = [torch.empty(B.compress_lz4_bound(cn, es, 0), dtype=torch.uint8, device=dev)
+                for _ in xs]
+        ys = [torch.empty_like(x) for x in xs]
+        state = {}
 
-    # parity gate before timing: exact round trip + consumed == produced
+        def step():
+            _, res = api.compress_lz4_batch_dev(xs, outs=outs, sync=False)
+            counts = res.cpu().tolist()  # the decoder needs the stream lengths
+            state["C"] = sum(counts)
+            api.decompress_lz4_batch_dev([o[:c] for o, c in zip(outs, counts)],
+                                         [x.shape for x in xs], dt, outs=ys, sync=False)
+
+        def check():
+            return all(torch.equal(x, y) for x, y in zip(xs, ys))
+        workload = ("batch of %d independent %d MiB %s G1 chunks per GPU (seed 12345 + global "
+                    "chunk id), default 8 KiB blocks, bshuf_*_lz4_batch_dev: one launch per kernel "
+                    "for all chunks, device-resident, decoder rebuilds each chunk's block index"
+                    % (nchunks, cfg["chunk_mib"], cfg["dtype"]))
+    elif cfg["what"] == "shuffle":
+        n = int(gib * GIB) // es
+        x = torch.empty(n, dtype=dt, device=dev)
+        B.synth_fill_dev(x, cfg["gen"], seed=12345 + rank)
+        nbytes = n * es
+        s_buf = torch.empty_like(x)
+        y = torch.empty_like(x)
+        state = {"C": 0}
+
+        def step():
+            api.bitshuffle_dev(x, out=s_buf)
+            api.bitunshuffle_dev(s_buf, out=y)
+
+        def check():
+            return torch.equal(x, y)
+        workload = ("bshuf_bitshuffle + bshuf_bitunshuffle of a %.3g MiB %s ramp (G0), default "
+                    "blocks, device-resident" % (nbytes / (1 << 20), cfg["dtype"]))
+    else:
+        n = int(gib * GIB) // es // 8 * 8
+        x = torch.empty(n, dtype=dt, device=dev)
+        B.synth_fill_dev(x, cfg["gen"], first=0, seed=12345 + rank)
+        nbytes = n * es
+        bound = B.compress_lz4_bound(n, es, 0)
+        comp = torch.empty(bound, dtype=torch.uint8, device=dev)
+        ws_enc = api.compress_lz4_workspace(n, es, 0, device=dev)
+        ws_dec = api.decompress_lz4_workspace(bound, n, es, 0, device=dev)
+        res_e = torch.empty(1, dtype=torch.int64, device=dev)
+        res_d = torch.empty(1, dtype=torch.int64, device=dev)
+        y = torch.empty_like(x)
+        state = {}
+
+        def step():
+            api.compress_lz4_dev(x, out=comp, workspace=ws_enc, result=res_e, sync=False)
+            c = int(res_e.item())  # the decoder needs the stream length on the host
+            state["C"] = c
+            api.decompress_lz4_dev(comp[:c], x.shape, x.dtype, out=y, workspace=ws_dec,
+                                   result=res_d, sync=False)
+
+        def check():
+            return int(res_d.item()) == state["C"] and torch.equal(x, y)
+        workload = ("bitshuffle+LZ4 encode+decode round trip, %.3g GiB %s %s per GPU, default "
+                    "blocks (%d elem), device-resident, decoder rebuilds the block index" % (
+                        gib, cfg["dtype"], "G1 correlated noise" if cfg["gen"] == 1
+                        else "G2 smooth field", B.default_block_size(es)))
+
+    # parity gate before timing: exact round trip
     step()
     torch.cuda.synchronize()
-    if int(res_d.item()) != clen[0] or not torch.equal(x, y):
+    if not check():
         raise SystemExit("round trip parity FAILED on rank %d" % rank)
 
-    lib = B.lib
     if not args.no_prof:
         lib.bshuf_prof_enable(1)
         prof_collect(lib)  # reset
@@ -213,8 +360,7 @@ def main(argv=None):
     if not args.no_prof:
         kern = prof_collect(lib)
         lib.bshuf_prof_enable(0)
-    # the warmup steps are also in the event log: count only per-launch averages
-    C = clen[0]
+    C = state["C"]
     total_bytes = sum_over_ranks(float(nbytes) * args.steps, world, dev)
     value = total_bytes / elapsed / GIB
     ms_step = elapsed / args.steps * 1e3
@@ -222,41 +368,50 @@ def main(argv=None):
     roofline = None
     kernels = {}
     if kern:
+        # algorithmic bytes per launch, SURVEY.md 8(d): encode N + C, decode
+        # C + N, transposes 2N (scratch / index traffic is not credited)
         alg = {"k_lz4_encode": nbytes + C, "k_lz4_decode": C + nbytes, "k_compact": C,
-               "k_idx_exits": C, "k_bitshuffle": 2 * nbytes, "k_bitunshuffle": 2 * nbytes}
+               "k_idx_exits": C, "k_seq_scan": C, "k_bitshuffle": 2 * nbytes,
+               "k_bitunshuffle": 2 * nbytes}
         for name, (cnt, ms) in kern.items():
             kernels[name] = round(ms / cnt, 4)
         dom = max(kern, key=lambda k: kern[k][1])
         avg_s = kern[dom][1] / kern[dom][0] / 1e3
         ach = alg.get(dom, nbytes + C) / avg_s / 1e9
         pmc = load_pmc_traffic()
-        traffic = pmc.get(dom) if isinstance(pmc, dict) else None
+        traffic = pmc.get(dom) if isinstance(pmc, dict) and args.config == 2 else None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "alg_bytes_per_launch": alg.get(dom, nbytes + C),
                     "avg_launch_ms": round(avg_s * 1e3, 4)}
-    # whole round trip priced as SURVEY.md 8(d): 2(N+C) algorithmic bytes per GPU
-    rt = 2.0 * (nbytes + C) * args.steps / elapsed / 1e9
+    # whole round trip priced as SURVEY.md 8(d): 2(N+C) algorithmic bytes per
+    # GPU for the codec, 4N for a transpose round trip
+    per_step = 4.0 * nbytes if cfg["what"] == "shuffle" else 2.0 * (nbytes + C)
+    rt = per_step * args.steps / elapsed / 1e9
     stage = {"alg_GBps_per_gpu": round(rt, 1), "roofline_frac": round(rt / HBM_PEAK_GBS, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(args.cpu_sample_mib)
+            cpu = cpu_baseline(args.cpu_sample_mib, cfg)
         except Exception as e:  # reported, never fatal for the GPU line
             cpu = {"value": None, "error": repr(e)}
 
     if rank == 0:
+        metric = METRIC if args.config == 2 else (
+            "device-resident GiB/s, BASELINE config %d (%s); %% HBM roofline" % (
+                args.config, {1: "bitshuffle+bitunshuffle 64 MiB int32",
+                              3: "bitshuffle+LZ4 encode+decode 16 GiB float32",
+                              4: "bitshuffle+LZ4 batch of 32 MiB int16 chunks"}[args.config]))
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "metric": metric, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": "bitshuffle+LZ4 encode+decode round trip, %.3g GiB int16 G1 "
-                                   "correlated noise per GPU, default 8 KiB blocks (4096 elem), "
-                                   "device-resident, decoder rebuilds the block index" % args.gib,
-                       "elem_size": 2, "block_size": 4096, "bytes_per_gpu": nbytes,
-                       "compressed_bytes_rank0": C, "ratio": round(nbytes / max(C, 1), 4),
+            "config": {"workload": workload, "baseline_config": args.config,
+                       "elem_size": es, "block_size": B.default_block_size(es),
+                       "bytes_per_gpu": nbytes, "compressed_bytes_rank0": C,
+                       "ratio": round(nbytes / C, 4) if C else None,
                        "parallelism": "shard-per-gpu x%d" % world},
             "roofline": roofline, "round_trip": stage, "kernels_avg_ms": kernels,
             "cpu_baseline": cpu,

@@ -70,4 +70,31 @@ def test_bench_collectives_world2():
 def test_bench_args_default_to_one_gpu():
     import bench
     a = bench.parse_args([])
-    assert a.gpus == 1 and a.steps >= 1 and a.warmup >= 0 and a.gib == 4.0
+    assert a.gpus == 1 and a.steps >= 1 and a.warmup >= 0 and a.config == 2
+    assert bench.CONFIGS[2]["gib"] == 4.0 and bench.CONFIGS[2]["dtype"] == "int16"
+
+
+def test_bench_gpus_spawns_ranks_and_checks_world(monkeypatch):
+    """--gpus N outside torch.distributed re-launches bench.py under
+    torch.distributed.run with N ranks (as a child process, exiting with its
+    status); inside, a world size that differs from --gpus is an error."""
+    import bench
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd, env=None: calls.append((cmd, env)) or 7)
+    with pytest.raises(SystemExit) as ei:
+        bench.maybe_spawn(bench.parse_args(["--gpus", "4", "--steps", "3"]), ["--gpus", "4", "--steps", "3"])
+    assert ei.value.code == 7
+    cmd, env = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-3:] == ["--gpus", "4", "--steps", "3"][-3:]
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # one GPU, or already inside torch.distributed: no re-launch
+    bench.maybe_spawn(bench.parse_args([]), [])
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    bench.maybe_spawn(bench.parse_args(["--gpus", "2"]), ["--gpus", "2"])
+    assert len(calls) == 1
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    with pytest.raises(SystemExit):
+        bench.dist_setup(bench.parse_args(["--gpus", "2"]))
