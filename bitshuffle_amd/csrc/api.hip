@@ -7,6 +7,7 @@
 // entry point returns -70.  The *_dev entry points take device pointers and
 // only enqueue work.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -503,6 +504,132 @@ int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first, 
 // host-pointer drop-in entry points
 // ---------------------------------------------------------------------------
 
+}  // extern "C"
+
+namespace {
+
+// Per-thread state of the host-pointer entry points: one HIP stream and
+// grow-only device buffers, so a caller that hands over chunk after chunk (the
+// HDF5 filter: one call per chunk) allocates nothing after the first call.
+// The buffers live until process exit (freeing device memory from a
+// thread-exit destructor could race the HIP runtime's own teardown).
+struct HostCtx {
+    enum { kIn, kOut, kWs, kOffs, kRes, kN };
+    void* buf[kN] = {};
+    size_t cap[kN] = {};
+    std::vector<uint64_t> offs;
+    // pinned double-buffered staging (host memcpy of piece i+1 overlaps the
+    // DMA of piece i); created on first use
+    void* pin[2] = {};
+    hipEvent_t ev[2] = {};
+    bool pending[2] = {};
+};
+
+HostCtx& host_ctx() {
+    thread_local HostCtx* c = new HostCtx();
+    return *c;
+}
+
+void* ctx_buf(int i, size_t n, hipStream_t s) {
+    HostCtx& c = host_ctx();
+    if (n == 0) n = 1;
+    if (c.buf[i] && c.cap[i] >= n) return c.buf[i];
+    if (c.buf[i]) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(c.buf[i]);
+        c.buf[i] = nullptr;
+        c.cap[i] = 0;
+    }
+    const size_t want = std::max(n, c.cap[i] + c.cap[i] / 4);
+    if (hipMalloc(&c.buf[i], want) != hipSuccess) {
+        c.buf[i] = nullptr;
+        return nullptr;
+    }
+    c.cap[i] = want;
+    return c.buf[i];
+}
+
+// Host <-> device copies go in pieces through two pinned staging buffers of
+// the thread: the host memcpy of one piece overlaps the DMA of the other.
+// Copying from a caller's pageable buffer directly makes the runtime pin its
+// pages on every call -- for the fresh per-chunk buffers HDF5 hands a filter
+// that costs more than the copy itself.  BSHUF_HOST_STAGING=0 copies directly.
+constexpr size_t kStagePiece = 8u << 20;
+
+bool staging_on() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("BSHUF_HOST_STAGING");
+        on = !(e && e[0] == '0');
+    }
+    return on != 0;
+}
+
+bool stage_init(HostCtx& c) {
+    for (int b = 0; b < 2; b++) {
+        if (!c.pin[b] && hipHostMalloc(&c.pin[b], kStagePiece, hipHostMallocDefault) != hipSuccess) {
+            c.pin[b] = nullptr;
+            return false;
+        }
+        if (!c.ev[b] && hipEventCreateWithFlags(&c.ev[b], hipEventDisableTiming) != hipSuccess) {
+            c.ev[b] = nullptr;
+            return false;
+        }
+    }
+    return true;
+}
+
+// Appends `n` bytes host -> device at dst (piece by piece; returns at once
+// after the last memcpy, the DMA may still run).
+hipError_t h2d(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s) {
+    HostCtx& c = host_ctx();
+    if (!staging_on() || !stage_init(c)) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
+    static thread_local int nb = 0;
+    for (size_t off = 0; off < n; off += kStagePiece) {
+        const size_t len = std::min(kStagePiece, n - off);
+        const int b = nb;
+        nb ^= 1;
+        if (c.pending[b] && hipEventSynchronize(c.ev[b]) != hipSuccess) return hipErrorUnknown;
+        memcpy(c.pin[b], src + off, len);
+        hipError_t e = hipMemcpyAsync(dst + off, c.pin[b], len, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipEventRecord(c.ev[b], s);
+        if (e != hipSuccess) return e;
+        c.pending[b] = true;
+    }
+    return hipSuccess;
+}
+
+// n bytes device -> host, completed on return (the DMA of piece i+1 overlaps
+// the host memcpy of piece i).
+hipError_t d2h(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s) {
+    HostCtx& c = host_ctx();
+    if (!staging_on() || !stage_init(c)) {
+        const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    }
+    for (int b = 0; b < 2; b++)
+        if (c.pending[b] && hipEventSynchronize(c.ev[b]) != hipSuccess) return hipErrorUnknown;
+    c.pending[0] = c.pending[1] = false;
+    const size_t npieces = (n + kStagePiece - 1) / kStagePiece;
+    auto issue = [&](size_t i) -> hipError_t {
+        const size_t off = i * kStagePiece, len = std::min(kStagePiece, n - off);
+        hipError_t e = hipMemcpyAsync(c.pin[i & 1], src + off, len, hipMemcpyDeviceToHost, s);
+        return e == hipSuccess ? hipEventRecord(c.ev[i & 1], s) : e;
+    };
+    if (npieces && issue(0) != hipSuccess) return hipErrorUnknown;
+    for (size_t i = 0; i < npieces; i++) {
+        if (i + 1 < npieces && issue(i + 1) != hipSuccess) return hipErrorUnknown;
+        if (hipEventSynchronize(c.ev[i & 1]) != hipSuccess) return hipErrorUnknown;
+        const size_t off = i * kStagePiece, len = std::min(kStagePiece, n - off);
+        memcpy(dst + off, c.pin[i & 1], len);
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
 static int64_t transpose_host(const void* in, void* out, size_t size, size_t elem_size,
                               size_t block_size, bool fwd) {
     Plan p;
@@ -512,13 +639,13 @@ static int64_t transpose_host(const void* in, void* out, size_t size, size_t ele
     const size_t bytes = size * elem_size;
     if (bytes == 0) return 0;
     hipStream_t s = thread_stream();
-    DevBuf di, dout;
-    if (di.alloc(bytes, s) != hipSuccess || dout.alloc(bytes, s) != hipSuccess) return -1;
-    if (hipMemcpyAsync(di.p, in, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return kErrHip;
-    const int64_t n = transpose_dev(di.p, dout.p, size, elem_size, block_size, s, fwd);
+    void* di = ctx_buf(HostCtx::kIn, bytes, s);
+    void* dout = ctx_buf(HostCtx::kOut, bytes, s);
+    if (!di || !dout) return -1;
+    if (h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) return kErrHip;
+    const int64_t n = transpose_dev(di, dout, size, elem_size, block_size, s, fwd);
     if (n < 0) return n;
-    if (hipMemcpyAsync(out, dout.p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return kErrHip;
-    if (hipStreamSynchronize(s) != hipSuccess) return kErrHip;
+    if (d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess) return kErrHip;
     return n;
 }
 
@@ -537,28 +664,28 @@ int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const s
     Plan p;
     const int64_t r = make_plan(size, elem_size, block_size, p);
     if (r) return r;
+    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
     if (!have_device()) return kErrHip;
     const size_t bytes = size * elem_size;
     const size_t bound = bshuf_compress_lz4_bound(size, elem_size, block_size);
+    const size_t wsb = bshuf_compress_lz4_dev_workspace(size, elem_size, block_size);
     hipStream_t s = thread_stream();
-    DevBuf di, dout, dres;
-    if (di.alloc(bytes, s) != hipSuccess || dout.alloc(bound, s) != hipSuccess ||
-        dres.alloc(8, s) != hipSuccess)
-        return -1;
-    if (bytes && hipMemcpyAsync(di.p, in, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-        return kErrHip;
-    const int64_t e = bshuf_compress_lz4_dev(di.p, dout.p, size, elem_size, block_size, nullptr, 0,
-                                             (int64_t*)dres.p, nullptr, s);
+    void* di = ctx_buf(HostCtx::kIn, bytes, s);
+    void* dout = ctx_buf(HostCtx::kOut, bound, s);
+    void* ws = ctx_buf(HostCtx::kWs, wsb, s);
+    int64_t* dres = (int64_t*)ctx_buf(HostCtx::kRes, 8, s);
+    if (!di || !dout || !ws || !dres) return -1;
+    if (bytes && h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) return kErrHip;
+    const int64_t e = bshuf_compress_lz4_dev(di, dout, size, elem_size, block_size, ws, wsb, dres,
+                                             nullptr, s);
     if (e < 0) return e;
     int64_t res = 0;
-    if (hipMemcpyAsync(&res, dres.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return kErrHip;
-    if (res > 0 && (size_t)res <= bound) {
-        if (hipMemcpyAsync(out, dout.p, (size_t)res, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return kErrHip;
-    }
+    if (res > 0 && (size_t)res <= bound &&
+        d2h((uint8_t*)out, (const uint8_t*)dout, (size_t)res, s) != hipSuccess)
+        return kErrHip;
     return res;
 }
 
@@ -569,17 +696,30 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const
     if (r) return r;
     if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
     if (!have_device()) return kErrHip;
+    const size_t bytes = size * elem_size;
+    hipStream_t s = thread_stream();
+    // The stream is at most the compress bound: stage into a buffer of that
+    // size while the walk below finds its real length.
+    const size_t max_in = bshuf_compress_lz4_bound(size, elem_size, block_size);
+    uint8_t* di = (uint8_t*)ctx_buf(HostCtx::kIn, max_in, s);
+    void* dout = ctx_buf(HostCtx::kOut, bytes, s);
+    uint64_t* doffs = (uint64_t*)ctx_buf(HostCtx::kOffs, (size_t)p.nb * 8, s);
+    int64_t* dres = (int64_t*)ctx_buf(HostCtx::kRes, 8, s);
+    if (!di || !dout || !doffs || !dres) return -1;
     // Walk the BE32 headers through the host buffer (the reference's own
     // iochain walk, src/bitshuffle.c:92-95) -- this also tells how many bytes
-    // of `in` belong to the stream, which the caller does not pass.
+    // of `in` belong to the stream, which the caller does not pass.  Every
+    // kStagePiece bytes walked leave for the device at once, so the copy
+    // overlaps the rest of the walk.
     // The walk stops at the first implausible header (length 0 or above
     // LZ4_compressBound of its block): that record is staged up to the bound,
     // the blocks behind it keep the all-ones "unresolved" offset, and the
     // device decoder assigns every error code (-1001 / -91 / -1YYY), exactly
     // as bshuf_decompress_lz4_dev does for the same bytes.
     const uint8_t* i8 = (const uint8_t*)in;
-    std::vector<uint64_t> offs((size_t)p.nb, ~(uint64_t)0);
-    uint64_t pos = 0;
+    std::vector<uint64_t>& offs = host_ctx().offs;
+    offs.assign((size_t)p.nb, ~(uint64_t)0);
+    uint64_t pos = 0, issued = 0;
     bool broken = false;
     for (int64_t k = 0; k < p.nb; k++) {
         offs[(size_t)k] = pos;
@@ -593,31 +733,26 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const
             break;
         }
         pos += 4 + (uint64_t)len;
+        if (pos - issued >= kStagePiece) {
+            if (h2d(di + issued, i8 + issued, (size_t)(pos - issued), s) != hipSuccess) return kErrHip;
+            issued = pos;
+        }
     }
     const size_t in_nbytes = (size_t)pos + (broken ? 0 : (size_t)p.tail);
-    const size_t bytes = size * elem_size;
-    hipStream_t s = thread_stream();
-    DevBuf di, dout, dres, doffs;
-    if (di.alloc(in_nbytes, s) != hipSuccess || dout.alloc(bytes, s) != hipSuccess ||
-        dres.alloc(8, s) != hipSuccess || doffs.alloc((size_t)p.nb * 8, s) != hipSuccess)
-        return -1;
-    if ((in_nbytes && hipMemcpyAsync(di.p, in, in_nbytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
-        (p.nb && hipMemcpyAsync(doffs.p, offs.data(), (size_t)p.nb * 8, hipMemcpyHostToDevice, s) !=
+    if (in_nbytes > max_in) return -91;
+    if ((in_nbytes > issued && h2d(di + issued, i8 + issued, in_nbytes - issued, s) != hipSuccess) ||
+        (p.nb && hipMemcpyAsync(doffs, offs.data(), (size_t)p.nb * 8, hipMemcpyHostToDevice, s) !=
                      hipSuccess))
         return kErrHip;
-    const int64_t e = bshuf_decompress_lz4_dev(di.p, in_nbytes, dout.p, size, elem_size, block_size,
-                                               nullptr, 0, (int64_t*)dres.p,
-                                               (const uint64_t*)doffs.p, s);
+    const int64_t e = bshuf_decompress_lz4_dev(di, in_nbytes, dout, size, elem_size, block_size,
+                                               nullptr, 0, dres, doffs, s);
     if (e < 0) return e;
     int64_t res = 0;
-    if (hipMemcpyAsync(&res, dres.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return kErrHip;
-    if (res >= 0 && bytes) {
-        if (hipMemcpyAsync(out, dout.p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return kErrHip;
-    }
+    if (res >= 0 && bytes && d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess)
+        return kErrHip;
     return res;
 }
 

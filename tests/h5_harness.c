@@ -13,6 +13,10 @@
  *     BASELINE config 5: uint16 (G1 + 32768) dataset written and read back
  *     through the filter (block 0, LZ4), verified, host-memory end to end;
  *     prints one JSON line with write/read GB/s.
+ *   h5_harness chunks <file.h5> <dataset>
+ *     Writes every stored (filtered) chunk of a 1-D dataset to stdout, raw, in
+ *     chunk order (H5Dread_chunk), for byte-for-byte / digest comparison with
+ *     the reference's u64BE || u32BE || bshuf_compress_lz4 chunk format.
  */
 #include <hdf5.h>
 #include <stdint.h>
@@ -45,17 +49,47 @@ static double now(void) {
     return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
-static hid_t make_dset(hid_t file, const char* name, hid_t type, hsize_t n, hsize_t chunk,
-                       unsigned block) {
+static hid_t make_dset_f(hid_t file, const char* name, hid_t type, hsize_t n, hsize_t chunk,
+                         unsigned block, int filtered) {
     hid_t space = H5Screate_simple(1, &n, NULL);
     hid_t dcpl = H5Pcreate(H5P_DATASET_CREATE);
     H5Pset_chunk(dcpl, 1, &chunk);
     const unsigned opts[2] = {block, 2 /* LZ4 */};
-    if (H5Pset_filter(dcpl, FILTER, H5Z_FLAG_MANDATORY, 2, opts) < 0) return -1;
+    if (filtered && H5Pset_filter(dcpl, FILTER, H5Z_FLAG_MANDATORY, 2, opts) < 0) return -1;
     hid_t d = H5Dcreate2(file, name, type, space, H5P_DEFAULT, dcpl, H5P_DEFAULT);
     H5Pclose(dcpl);
     H5Sclose(space);
     return d;
+}
+
+static hid_t make_dset(hid_t file, const char* name, hid_t type, hsize_t n, hsize_t chunk,
+                       unsigned block) {
+    return make_dset_f(file, name, type, n, chunk, block, 1);
+}
+
+/* The same chunked write + read with NO filter: HDF5's own I/O floor on this
+ * machine (chunk copies, file writes/reads), for reading the filtered rates. */
+static void io_floor(const char* out, const uint16_t* a, uint16_t* b, long long n, long long chunk,
+                     double* w, double* r) {
+    char path[1100];
+    snprintf(path, sizeof path, "%s.raw", out);
+    hid_t file = H5Fcreate(path, H5F_ACC_TRUNC, H5P_DEFAULT, H5P_DEFAULT);
+    hid_t d = make_dset_f(file, "data", H5T_NATIVE_UINT16, (hsize_t)n, (hsize_t)chunk, 0, 0);
+    double t0 = now();
+    H5Dwrite(d, H5T_NATIVE_UINT16, H5S_ALL, H5S_ALL, H5P_DEFAULT, a);
+    H5Dclose(d);
+    H5Fclose(file);
+    double t1 = now();
+    file = H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT);
+    d = H5Dopen2(file, "data", H5P_DEFAULT);
+    double t2 = now();
+    H5Dread(d, H5T_NATIVE_UINT16, H5S_ALL, H5S_ALL, H5P_DEFAULT, b);
+    double t3 = now();
+    H5Dclose(d);
+    H5Fclose(file);
+    remove(path);
+    *w = n * 2 / (t1 - t0) / 1e9;
+    *r = n * 2 / (t3 - t2) / 1e9;
 }
 
 static int regress(const char* dir, const char* out) {
@@ -150,15 +184,54 @@ static int roundtrip(const char* out, long long n, long long chunk) {
     H5Dclose(d);
     H5Fclose(file);
     const int same = memcmp(a, b, (size_t)n * 2) == 0;
+    double fw = 0, fr = 0;
+    if (getenv("BSHUF_H5_IO_FLOOR")) io_floor(out, a, b, n, chunk, &fw, &fr);
     printf("{\"config\": \"hdf5 filter 32008 uint16 G1+32768\", \"bytes\": %lld, \"chunk_bytes\": %lld, "
-           "\"stored_bytes\": %llu, \"write_GBps\": %.3f, \"read_GBps\": %.3f, \"match\": %s}\n",
+           "\"stored_bytes\": %llu, \"write_GBps\": %.3f, \"read_GBps\": %.3f, "
+           "\"nofilter_write_GBps\": %.3f, \"nofilter_read_GBps\": %.3f, \"match\": %s}\n",
            n * 2, chunk * 2, (unsigned long long)stored, n * 2 / (t1 - t0) / 1e9,
-           n * 2 / (t3 - t2) / 1e9, same ? "true" : "false");
+           n * 2 / (t3 - t2) / 1e9, fw, fr, same ? "true" : "false");
     free(a), free(b);
     return same ? 0 : 1;
 }
 
+static int chunks(const char* path, const char* name) {
+    hid_t file = H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT);
+    if (file < 0) return 2;
+    hid_t d = H5Dopen2(file, name, H5P_DEFAULT);
+    if (d < 0) return 3;
+    hid_t space = H5Dget_space(d);
+    hsize_t n = 0, chunk = 0;
+    H5Sget_simple_extent_dims(space, &n, NULL);
+    hid_t dcpl = H5Dget_create_plist(d);
+    if (H5Pget_chunk(dcpl, 1, &chunk) != 1 || chunk == 0) return 4;
+    size_t cap = 0;
+    unsigned char* buf = NULL;
+    for (hsize_t o = 0; o < n; o += chunk) {
+        hsize_t off[1] = {o}, sz = 0;
+        uint32_t fm = 0;
+        if (H5Dget_chunk_storage_size(d, off, &sz) < 0) return 5;
+        if (sz > cap) {
+            free(buf);
+            cap = (size_t)sz;
+            buf = malloc(cap);
+            if (!buf) return 6;
+        }
+        if (H5Dread_chunk(d, H5P_DEFAULT, off, &fm, buf) < 0) return 7;
+        if (fwrite(buf, 1, (size_t)sz, stdout) != (size_t)sz) return 8;
+        fprintf(stderr, "chunk %llu %llu\n", (unsigned long long)o, (unsigned long long)sz);
+    }
+    fflush(stdout);
+    free(buf);
+    H5Pclose(dcpl);
+    H5Sclose(space);
+    H5Dclose(d);
+    H5Fclose(file);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 4 && !strcmp(argv[1], "chunks")) return chunks(argv[2], argv[3]);
     if (argc == 4 && !strcmp(argv[1], "regress")) return regress(argv[2], argv[3]);
     if (argc == 5 && !strcmp(argv[1], "roundtrip"))
         return roundtrip(argv[2], atoll(argv[3]), atoll(argv[4]));
