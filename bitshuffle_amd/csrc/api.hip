@@ -85,6 +85,11 @@ size_t enc_ws(const Plan& p, EncodeBufs* b, uint8_t* base) {
     x.offs = c.take<uint64_t>((size_t)(p.nb + 1) * 8);
     x.scan_tmp_bytes = encode_scan_tmp_bytes(p.nb);
     x.scan_tmp = c.take<void>(x.scan_tmp_bytes);
+    if ((int64_t)p.L.bs * p.L.E > max_lds_encode_bytes()) {
+        // large blocks: bit-transposed copy (+ over-read pad) and LZ4 tables
+        x.shuf = c.take<uint8_t>((size_t)(p.L.nfull * (int64_t)p.L.bs + p.L.last) * p.L.E + 64);
+        x.tables = c.take<uint32_t>((size_t)p.nb * kLargeTableWords * 4);
+    }
     if (b) *b = x;
     return c.off;
 }
@@ -106,6 +111,8 @@ size_t dec_ws(const Plan& p, int64_t blocks_end, int64_t in_nbytes, bool need_in
     x.bad = c.take<long long>(8);
     x.scan_tmp_bytes = need_index ? decode_scan_tmp_bytes(x.nchunks) : 0;
     x.scan_tmp = c.take<void>(x.scan_tmp_bytes + 8);
+    if ((int64_t)p.L.bs * p.L.E > max_lds_decode_bytes())
+        x.shuf = c.take<uint8_t>((size_t)(p.L.nfull * (int64_t)p.L.bs + p.L.last) * p.L.E + 64);
     if (b) *b = x;
     return c.off;
 }
@@ -200,7 +207,6 @@ int64_t bshuf_compress_lz4_dev(const void* in, void* out, size_t size, size_t el
     Plan p;
     const int64_t r = make_plan(size, elem_size, block_size, p);
     if (r) return r;
-    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
     if (!have_device()) return kErrHip;
     hipStream_t s = (hipStream_t)stream;
     const size_t need = enc_ws(p, nullptr, nullptr);
@@ -238,7 +244,6 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
     Plan p;
     const int64_t r = make_plan(size, elem_size, block_size, p);
     if (r) return r;
-    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
     if (!have_device()) return kErrHip;
     hipStream_t s = (hipStream_t)stream;
     int64_t cb = (int64_t)in_nbytes - p.tail;
@@ -315,7 +320,6 @@ int64_t make_batch(const void* const* in, void* const* out, const size_t* sizes,
         bp.nchunks += g.nchunks;
         bp.seq_words += g.in_nbytes / 3 + 80;
     }
-    if ((int64_t)bp.L.bs * bp.L.E > max_device_block_bytes()) return kErrUnsupported;
     bp.L.nfull = bp.nb;
     bp.L.last = 0;
     return 0;
@@ -429,7 +433,7 @@ int64_t bshuf_compress_lz4_batch_dev(const void* const* in, void* const* out, co
     // blocks of both LZ4 table types in one batch (a byU32-size block_size
     // with a byU16-size partial block): one stream at a time
     const bool wide = (int64_t)bp.L.bs * bp.L.E >= kU16TableLimit;
-    bool mixed = false;
+    bool mixed = (int64_t)bp.L.bs * bp.L.E > max_lds_encode_bytes();  // large blocks: per stream
     for (const Seg& g : bp.segs) mixed = mixed || (g.last && ((int64_t)g.last * bp.L.E >= kU16TableLimit) != wide);
     if (mixed) {
         for (size_t i = 0; i < count; i++) {
@@ -474,6 +478,16 @@ int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_n
     if (!have_device()) return kErrHip;
     hipStream_t s = (hipStream_t)stream;
     for (size_t i = 0; i < count; i++) bp.segs[i].result = d_results + i;
+    if ((int64_t)bp.L.bs * bp.L.E > max_lds_decode_bytes()) {
+        // blocks above the LDS decoder's size: one stream at a time
+        for (size_t i = 0; i < count; i++) {
+            const int64_t e = bshuf_decompress_lz4_dev(in[i], in_nbytes[i], out[i], sizes[i], elem_size,
+                                                       block_size, nullptr, 0, d_results + i, nullptr,
+                                                       stream);
+            if (e) return e;
+        }
+        return 0;
+    }
     DevBuf own;
     const size_t need = dec_batch_ws(bp, nullptr, nullptr, nullptr, nullptr, nullptr);
     const int64_t w = get_ws(ws, ws_bytes, need, own, s);
@@ -696,7 +710,6 @@ int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const s
     Plan p;
     const int64_t r = make_plan(size, elem_size, block_size, p);
     if (r) return r;
-    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
     if (!have_device()) return kErrHip;
     const size_t bytes = size * elem_size;
     const size_t bound = bshuf_compress_lz4_bound(size, elem_size, block_size);
@@ -726,7 +739,6 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const
     Plan p;
     const int64_t r = make_plan(size, elem_size, block_size, p);
     if (r) return r;
-    if ((int64_t)p.L.bs * p.L.E > max_device_block_bytes()) return kErrUnsupported;
     if (!have_device()) return kErrHip;
     const size_t bytes = size * elem_size;
     hipStream_t s = thread_stream();

@@ -71,6 +71,8 @@ struct EncodeBufs {
     uint64_t* offs;     // nblocks + 1 u64: exclusive scan of foot
     void* scan_tmp;     // hipcub temp storage
     size_t scan_tmp_bytes;
+    uint8_t* shuf = nullptr;     // large blocks: the bit-transposed input
+    uint32_t* tables = nullptr;  // large blocks: kLargeTableWords per block
 };
 size_t encode_scan_tmp_bytes(int64_t nblocks);
 int64_t encode_slot_bytes(const Layout& L);
@@ -84,8 +86,14 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
 hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
                                const Layout& L, const EncodeBufs& b, uint64_t* block_offsets,
                                hipStream_t s);
-// Largest block (bytes) the LDS-resident encoder/decoder accepts.
+// Largest block (bytes) the LDS-resident encoder accepts.
 int64_t max_device_block_bytes();
+// Blocks above these sizes take the global-memory path (lz4_large.hip).
+int64_t max_lds_encode_bytes();
+int64_t max_lds_decode_bytes();
+constexpr int64_t kLargeTableWords = 8192;
+hipError_t launch_encode_large(const uint8_t* in, const Layout& L, const EncodeBufs& b,
+                               uint8_t* shuf, uint32_t* tables, hipStream_t s);
 
 // ---- LZ4 decode --------------------------------------------------------
 struct DecodeBufs {
@@ -102,6 +110,7 @@ struct DecodeBufs {
     size_t scan_tmp_bytes;
     int64_t chunk;      // chunk bytes for the index rebuild
     int64_t nchunks;
+    uint8_t* shuf = nullptr;  // large blocks: decoded, still bit-transposed
 };
 int64_t index_chunk_bytes(const Layout& L);
 size_t decode_scan_tmp_bytes(int64_t nchunks);
@@ -110,6 +119,8 @@ hipError_t launch_index(const uint8_t* in, int64_t blocks_end, const Layout& L,
 hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
                          hipStream_t s);
+hipError_t launch_decode_large(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
+                               const DecodeBufs& b, uint8_t* shuf, hipStream_t s);
 // Batch versions: L.nfull = total blocks; b.idx_err and b.bad hold one word
 // per stream; chunk_seg / blk_seg map global chunks / blocks to streams.
 hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_seg, const Layout& L,

@@ -835,6 +835,12 @@ hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_
 
 namespace {
 
+hipError_t scan_impl(DecArgs& a, int64_t nb, hipStream_t s) {
+    ProfScope prof("k_seq_scan", s);
+    hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, a, nb);
+    return hipGetLastError();
+}
+
 // Scan + decode kernels over nb blocks (one stream, or all streams of a batch).
 hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     const Layout& L = a.L;
@@ -861,13 +867,8 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
         default: fn = BSHUF_DEC(0, 0); break;
     }
 #undef BSHUF_DEC
-    hipError_t e;
-    {
-        ProfScope prof("k_seq_scan", s);
-        hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, a, nb);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
+    hipError_t e = scan_impl(a, nb, s);
+    if (e != hipSuccess) return e;
     if (lds > 65536) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -910,7 +911,13 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
                   (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr};
-        e = decode_impl(a, nb, ((uintptr_t)out & 15) == 0, s);
+        if (nmax > max_lds_decode_bytes()) {
+            // large blocks: validated by the same scan, executed in global memory
+            e = scan_impl(a, nb, s);
+            if (e == hipSuccess) e = launch_decode_large(in, in_nbytes, out, L, b, b.shuf, s);
+        } else {
+            e = decode_impl(a, nb, ((uintptr_t)out & 15) == 0, s);
+        }
         if (e != hipSuccess) return e;
     }
     uint8_t* tail_dst = out + (L.nfull * (int64_t)L.bs + L.last) * L.E;

@@ -1001,7 +1001,10 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
                          const EncodeBufs& b, int64_t* d_result, hipStream_t s) {
     const int64_t nb = L.nblocks();
     hipError_t e;
-    if (nb > 0) {
+    if (nb > 0 && (int64_t)L.bs * L.E > max_lds_encode_bytes()) {
+        e = launch_encode_large(in, L, b, b.shuf, b.tables, s);
+        if (e != hipSuccess) return e;
+    } else if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
         const bool wide = nmax >= kU16TableLimit;
         // sequence descriptors behind the block when the record fits the

@@ -492,3 +492,49 @@ def test_batch_config4_digests(bs, torch):
     dec = bs.decompress_lz4_batch_dev(outs, [x.shape for x in xs], torch.int16)
     for x, d in zip(xs, dec):
         assert torch.equal(x, d)
+
+
+# ------------------------------------------------------------------ large blocks
+@pytest.mark.parametrize("block_bytes", [96 << 10, 143 << 10, 256 << 10, 1 << 20])
+def test_large_blocks_match_oracle(bs, oracle, torch, block_bytes):
+    """Every block size the reference accepts (any multiple of 8 elements,
+    src/bitshuffle_core.c:1894-1897): blocks above the LDS-resident kernels'
+    budget (decoder from ~81 KiB, encoder from ~144 KiB) take the global-memory
+    path; streams equal the oracle's and decode back, through the host API,
+    the device API (with the parallel index rebuild) and the batch API."""
+    rng = np.random.default_rng(block_bytes & 0xFFFF)
+    for E, dt in [(2, np.int16), (8, np.uint64), (1, np.uint8)]:
+        block = block_bytes // E
+        n = 2 * block + block // 3 // 8 * 8 + 5
+        if E == 2:
+            a = oracle.gen_g1(n, 77, 999)
+        else:
+            a = (rng.integers(-3, 4, n * E).cumsum() % 251).astype(np.uint8).view(dt)
+        want = oracle.compress_lz4(a, block)
+        got = bs.compress_lz4(a, block)
+        assert got.tobytes() == want.tobytes(), (E, block)
+        back = bs.decompress_lz4(want, a.shape, a.dtype, block)
+        assert back.tobytes() == a.tobytes(), (E, block)
+        t = torch.from_numpy(a.view(np.uint8).copy()).cuda()  # raw bytes: the C-ABI gets E
+        import ctypes
+        out = torch.empty(bs.compress_lz4_bound(a.size, E, block), dtype=torch.uint8, device="cuda")
+        res = torch.empty(1, dtype=torch.int64, device="cuda")
+        rc = bs.lib.bshuf_compress_lz4_dev(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                           a.size, E, block, None, 0, ctypes.c_void_p(res.data_ptr()),
+                                           None, None)
+        assert rc == 0 and int(res.item()) == want.size, (E, block)
+        assert out[:want.size].cpu().numpy().tobytes() == want.tobytes()
+        dec = torch.empty(a.nbytes, dtype=torch.uint8, device="cuda")
+        rc = bs.lib.bshuf_decompress_lz4_dev(ctypes.c_void_p(out.data_ptr()), want.size,
+                                             ctypes.c_void_p(dec.data_ptr()), a.size, E, block, None, 0,
+                                             ctypes.c_void_p(res.data_ptr()), None, None)
+        assert rc == 0 and int(res.item()) == want.size, (E, block, int(res.item()))
+        assert dec.cpu().numpy().tobytes() == a.view(np.uint8).tobytes(), (E, block)
+    # batch API (falls back to one stream at a time for such blocks)
+    xs = [torch.from_numpy(oracle.gen_g1(3 * (block_bytes // 2) + 11, i, 5 + i)).cuda() for i in range(2)]
+    outs = bs.compress_lz4_batch_dev(xs, block_bytes // 2)
+    for x, o in zip(xs, outs):
+        assert o.cpu().numpy().tobytes() == oracle.compress_lz4(x.cpu().numpy(), block_bytes // 2).tobytes()
+    dec = bs.decompress_lz4_batch_dev(outs, [x.shape for x in xs], torch.int16, block_bytes // 2)
+    for x, d in zip(xs, dec):
+        assert torch.equal(x, d)
