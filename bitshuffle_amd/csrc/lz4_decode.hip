@@ -66,6 +66,7 @@ struct IdxArgs {
     int64_t CH;          // chunk bytes
     int64_t W;           // candidate window (largest record)
     uint32_t maxlen;
+    int64_t win_lds;     // k_idx_exits' LDS window bytes
 };
 
 struct ChunkLoc {
@@ -103,7 +104,9 @@ __device__ __forceinline__ ChunkLoc chunk_loc(const IdxArgs& x, int64_t c) {
 }
 
 __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict__ exits) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kIdxWinMax + 64];
+    // the candidate window (largest record + 4, +64 slack), sized at launch:
+    // the chases below are latency-bound, so a small window buys residency
+    extern __shared__ __attribute__((aligned(16))) uint8_t win[];
     int win_off = 0;
     const int lane = threadIdx.x;
     const ChunkLoc L = chunk_loc(x, blockIdx.x);
@@ -115,17 +118,17 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
     const int64_t ce = min(cs + CH, Cb);
     const int64_t cend = (s == 0) ? cs + 1 : min(cs + W, Cb);  // candidate window
     const int64_t wbytes = min(cend + 3, Cb) - cs;
-    const bool use_lds = wbytes <= kIdxWinMax;
+    // 16-byte loads of the candidate window, aligned on the ABSOLUTE address:
+    // an aligned granule never crosses a page, so the bytes it reads outside
+    // [cs, cs+wbytes) cannot fault and are never used
+    const uintptr_t start = (uintptr_t)(in + cs);
+    const int sh = (int)(start & 15);
+    const int64_t nch = (sh + wbytes + 15) >> 4;
+    const bool use_lds = nch * 16 <= x.win_lds;
     if (use_lds) {
-        // 16-byte loads of the candidate window, aligned on the ABSOLUTE
-        // address: an aligned granule never crosses a page, so the bytes it
-        // reads outside [cs, cs+wbytes) cannot fault and are never used
-        const uintptr_t start = (uintptr_t)(in + cs);
         const gbl128c* g4 = g128_aligned_down(in + cs);
-        const int sh = (int)(start & 15);
-        const int nch = (sh + (int)wbytes + 15) >> 4;
         lds128* w4 = (lds128*)to_lds(win);
-        for (int c = lane; c < nch; c += kWave) w4[c] = g4[c];
+        for (int c = lane; c < (int)nch; c += kWave) w4[c] = g4[c];
         __syncthreads();
         win_off = sh;
     }
@@ -778,6 +781,14 @@ size_t decode_scan_tmp_bytes(int64_t nchunks) {
 
 namespace {
 
+// LDS of k_idx_exits: the candidate window of the largest record (+ 3 bytes
+// of the last header, + 16-byte alignment slack), capped at kIdxWinMax (a
+// larger window reads its candidates from global memory instead).
+int64_t idx_win_lds(uint32_t maxlen) {
+    const int64_t w = ((4 + (int64_t)maxlen + 3 + 16 + 64) + 15) & ~(int64_t)15;
+    return w < kIdxWinMax ? w : kIdxWinMax;
+}
+
 // Index rebuild over nch chunks (of one stream, or of every stream of a batch).
 hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, const DecodeBufs& b,
                       hipStream_t s) {
@@ -789,7 +800,13 @@ hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, cons
     if (e != hipSuccess || nch == 0) return e;
     {
         ProfScope prof("k_idx_exits", s);
-        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), 0, s, x, b.exits);
+        const size_t lds = (size_t)x.win_lds;
+        if (lds > 65536) {
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_idx_exits),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), lds, s, x, b.exits);
     }
     const unsigned wg = (unsigned)((nch + 63) / 64);
     {
@@ -821,7 +838,7 @@ hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const De
                         hipStream_t s) {
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     IdxArgs x{in, Cb, L.nblocks(), b.idx_err, nullptr, nullptr, nullptr, b.chunk,
-              4 + (int64_t)maxlen, maxlen};
+              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen)};
     return index_impl(x, L.nblocks(), b.nchunks, 1, b, s);
 }
 
@@ -829,7 +846,7 @@ hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_
                               int64_t nchunks, const DecodeBufs& b, hipStream_t s) {
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     IdxArgs x{nullptr, 0, L.nfull, nullptr, segs, chunk_seg, b.idx_err, b.chunk,
-              4 + (int64_t)maxlen, maxlen};
+              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen)};
     return index_impl(x, L.nfull, nchunks, nsegs, b, s);
 }
 

@@ -817,12 +817,17 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 // Destination 16-byte chunks fully inside the record are composed from five
 // source dwords with v_alignbyte and stored whole; the <= 2 edge chunks per
 // record use byte stores (they share dwords with the neighbouring records).
+// One WAVE per record, four records per 256-thread workgroup.
+constexpr int kCompactPerWg = 4;
+
 __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scratch, int64_t slot,
                                                  const uint64_t* __restrict__ offs,
                                                  uint8_t* __restrict__ out, const Seg* segs,
                                                  const uint32_t* __restrict__ blk_seg,
-                                                 uint64_t* __restrict__ block_offsets) {
-    const int64_t blk = blockIdx.x;
+                                                 uint64_t* __restrict__ block_offsets, int64_t nb) {
+    const int64_t blk = (int64_t)blockIdx.x * kCompactPerWg + (threadIdx.x >> 6);
+    const int tid = threadIdx.x & 63;
+    if (blk >= nb) return;
     uint64_t rel0 = offs[blk];
     const int64_t len = (int64_t)(offs[blk + 1] - rel0);
     if (segs) {  // batch: offsets are relative to the block's own stream
@@ -830,13 +835,13 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
         rel0 -= offs[g.first];
         out = g.out;
     }
-    if (block_offsets && threadIdx.x == 0) block_offsets[blk] = rel0;
+    if (block_offsets && tid == 0) block_offsets[blk] = rel0;
     const uint8_t* rec = scratch + blk * slot;
     const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(rec);
     // 16-byte chunks of the ABSOLUTE destination address space
     const uintptr_t dst0 = (uintptr_t)(out + rel0);
     const uintptr_t q0 = dst0 >> 4, q1 = (dst0 + (uintptr_t)len + 15) >> 4;
-    for (uintptr_t q = q0 + threadIdx.x; q < q1; q += 256) {
+    for (uintptr_t q = q0 + tid; q < q1; q += kWave) {
         const int64_t s = (int64_t)(q * 16 - dst0);  // record offset of the chunk's first byte
         gbl8* d = (gbl8*)(q * 16);
         if (s >= 0 && s + 16 <= len) {
@@ -1060,9 +1065,9 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
     if (e != hipSuccess) return e;
     if (nb > 0) {
         ProfScope prof("k_compact", s);
-        hipLaunchKernelGGL(k_compact, dim3((unsigned)nb), dim3(256), 0, s, b.scratch, b.slot,
-                           b.offs, out, (const Seg*)nullptr, (const uint32_t*)nullptr,
-                           (uint64_t*)nullptr);
+        hipLaunchKernelGGL(k_compact, dim3((unsigned)((nb + kCompactPerWg - 1) / kCompactPerWg)),
+                           dim3(256), 0, s, b.scratch, b.slot, b.offs, out, (const Seg*)nullptr,
+                           (const uint32_t*)nullptr, (uint64_t*)nullptr, nb);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1117,8 +1122,9 @@ hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
     if (e != hipSuccess) return e;
     if (nb > 0) {
         ProfScope prof("k_compact", s);
-        hipLaunchKernelGGL(k_compact, dim3((unsigned)nb), dim3(256), 0, s, b.scratch, b.slot, b.offs,
-                           (uint8_t*)nullptr, segs, blk_seg, block_offsets);
+        hipLaunchKernelGGL(k_compact, dim3((unsigned)((nb + kCompactPerWg - 1) / kCompactPerWg)),
+                           dim3(256), 0, s, b.scratch, b.slot, b.offs, (uint8_t*)nullptr, segs,
+                           blk_seg, block_offsets, nb);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
