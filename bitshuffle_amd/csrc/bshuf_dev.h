@@ -155,6 +155,55 @@ __device__ __forceinline__ void scatter_byte_plane(uint32_t (&w)[2 * EK], int b,
     }
 }
 
+// Bit-sliced inverse transpose of FOUR consecutive groups (4q .. 4q+3) of a
+// block: pl[r] holds byte (4q + k) of plane r in its byte k (one LDS dword per
+// plane).  The 8x8 bit transposes of all four groups run at once, as three
+// swap stages between plane registers (bits of one byte never leave it):
+// after them x[8b + i] byte k = byte b of element 8(4q + k) + i.  out[] gets
+// the 32 * EK contiguous output bytes of the four groups.
+template <int EK>
+__device__ __forceinline__ void untranspose4(const uint32_t (&pl)[8 * EK], uint32_t (&out)[8 * EK]) {
+    uint32_t x[8 * EK];
+#pragma unroll
+    for (int r = 0; r < 8 * EK; r++) x[r] = pl[r];
+#pragma unroll
+    for (int b = 0; b < EK; b++) {
+        uint32_t* y = x + 8 * b;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {  // swap bit 1<->0 blocks of rows j, j+1
+            const uint32_t t = ((y[j] >> 1) ^ y[j + 1]) & 0x55555555u;
+            y[j + 1] ^= t;
+            y[j] ^= t << 1;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {  // rows j, j+2
+            if (j & 2) continue;
+            const uint32_t t = ((y[j] >> 2) ^ y[j + 2]) & 0x33333333u;
+            y[j + 2] ^= t;
+            y[j] ^= t << 2;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {  // rows j, j+4
+            const uint32_t t = ((y[j] >> 4) ^ y[j + 4]) & 0x0F0F0F0Fu;
+            y[j + 4] ^= t;
+            y[j] ^= t << 4;
+        }
+    }
+    // output byte o = (8k + i) * EK + b  <-  x[8b + i] byte k
+#pragma unroll
+    for (int w = 0; w < 8 * EK; w++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int o = 4 * w + t;
+            const int b = o % EK, e = o / EK;
+            const int k = e >> 3, i = e & 7;
+            v |= ((x[8 * b + i] >> (8 * k)) & 0xFFu) << (8 * t);
+        }
+        out[w] = v;
+    }
+}
+
 template <int EK>
 __device__ __forceinline__ void load_group(const uint8_t* p, uint32_t (&w)[2 * EK]) {
     if constexpr (EK == 1) {

@@ -697,7 +697,22 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         if (status == 0 && !(VAR & 8)) {
             uint8_t* dst = cur.loc.out;
             if constexpr (EK != 0) {
-                for (int g = lane; g < P; g += kWave) {
+                // four groups per lane (EK <= 4; 8-byte elements would hold
+                // 192 registers): one LDS dword per plane, the bit-sliced
+                // transpose of untranspose4, 32*EK contiguous bytes out
+                const int P4 = (EK <= 4 && (P & 3) == 0) ? P >> 2 : 0;
+                const lds32* D32 = (const lds32*)D;
+                for (int q = lane; q < P4; q += kWave) {
+                    uint32_t pl[8 * EK], ob[8 * EK];
+#pragma unroll
+                    for (int r = 0; r < 8 * EK; r++) pl[r] = D32[r * P4 + q];
+                    untranspose4<EK>(pl, ob);
+                    uint4* o4 = reinterpret_cast<uint4*>(dst + (int64_t)q * 32 * EK);
+#pragma unroll
+                    for (int v = 0; v < 2 * EK; v++)
+                        o4[v] = make_uint4(ob[4 * v], ob[4 * v + 1], ob[4 * v + 2], ob[4 * v + 3]);
+                }
+                for (int g = (P4 ? P : lane); g < P; g += kWave) {
                     uint32_t w[2 * EK];
 #pragma unroll
                     for (int i = 0; i < 2 * EK; i++) w[i] = 0;
