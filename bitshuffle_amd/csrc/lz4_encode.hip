@@ -814,11 +814,38 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 }
 
 // Move each [BE32 c][c bytes] record from its scratch slot to out + offs[k].
-// Destination 16-byte chunks fully inside the record are composed from five
-// source dwords with v_alignbyte and stored whole; the <= 2 edge chunks per
-// record use byte stores (they share dwords with the neighbouring records).
-// One WAVE per record, four records per 256-thread workgroup.
+// Every lane owns 16-byte chunks of the ABSOLUTE destination address space:
+// it reads the two 16-aligned source granules under its chunk (the shift
+// between source and destination is the same for every chunk of a record, so
+// the dword select is wave-uniform), composes the chunk with v_alignbyte and
+// stores it whole -- or, for the <= 2 edge chunks a record shares with its
+// neighbours, byte by byte from the same registers.  Up to kCompactUnroll
+// chunks per lane are loaded before any is stored.  One WAVE per record, four
+// records per 256-thread workgroup.
 constexpr int kCompactPerWg = 4;
+constexpr int kCompactUnroll = 4;
+
+// 16 bytes at byte offset t (0..15, wave-uniform) of the 32-byte pair a|b.
+__device__ __forceinline__ u32x4 pair_bytes(const u32x4 a, const u32x4 b, int t) {
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t sh = (uint32_t)(t & 3);
+    u32x4 v;
+    switch (t >> 2) {
+#define BSHUF_PAIR(D)                                                                          \
+    case D:                                                                                     \
+        v = u32x4{__builtin_amdgcn_alignbyte(w[D + 1], w[D], sh),                               \
+                  __builtin_amdgcn_alignbyte(w[D + 2], w[D + 1], sh),                           \
+                  __builtin_amdgcn_alignbyte(w[D + 3], w[D + 2], sh),                           \
+                  __builtin_amdgcn_alignbyte(w[D + 4], w[D + 3], sh)};                          \
+        break;
+        BSHUF_PAIR(0)
+        BSHUF_PAIR(1)
+        BSHUF_PAIR(2)
+        default: BSHUF_PAIR(3)
+#undef BSHUF_PAIR
+    }
+    return v;
+}
 
 __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scratch, int64_t slot,
                                                  const uint64_t* __restrict__ offs,
@@ -836,29 +863,42 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
         out = g.out;
     }
     if (block_offsets && tid == 0) block_offsets[blk] = rel0;
-    const uint8_t* rec = scratch + blk * slot;
-    const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(rec);
-    // 16-byte chunks of the ABSOLUTE destination address space
+    // the slot is 16-aligned and 16 bytes longer than any record
+    const gbl128c* rec16 = (const gbl128c*)(scratch + blk * slot);
     const uintptr_t dst0 = (uintptr_t)(out + rel0);
-    const uintptr_t q0 = dst0 >> 4, q1 = (dst0 + (uintptr_t)len + 15) >> 4;
-    for (uintptr_t q = q0 + tid; q < q1; q += kWave) {
-        const int64_t s = (int64_t)(q * 16 - dst0);  // record offset of the chunk's first byte
-        gbl8* d = (gbl8*)(q * 16);
-        if (s >= 0 && s + 16 <= len) {
-            const int64_t w0 = s >> 2;
-            const uint32_t sh = (uint32_t)(s & 3);
-            uint32_t x[5];
+    const int64_t nq = (int64_t)(((dst0 + (uintptr_t)len + 15) >> 4) - (dst0 >> 4));
+    // chunk j starts at record byte s = 16 j - m: granules j - (m != 0) and
+    // the next one, byte offset t in the pair
+    const int m = (int)(dst0 & 15);
+    const int gshift = m ? 1 : 0, t = m ? 16 - m : 0;
+    gbl8* const d0 = (gbl8*)(dst0 & ~(uintptr_t)15);
+    for (int64_t jb = 0; jb < nq; jb += kWave * kCompactUnroll) {
+        u32x4 A[kCompactUnroll], Bv[kCompactUnroll];
 #pragma unroll
-            for (int i = 0; i < 5; i++) x[i] = rec32[w0 + i];
-            const u32x4 v = {__builtin_amdgcn_alignbyte(x[1], x[0], sh),
-                             __builtin_amdgcn_alignbyte(x[2], x[1], sh),
-                             __builtin_amdgcn_alignbyte(x[3], x[2], sh),
-                             __builtin_amdgcn_alignbyte(x[4], x[3], sh)};
-            *(gbl128*)d = v;
-        } else {
-            for (int i = 0; i < 16; i++) {
-                const int64_t r = s + i;
-                if (r >= 0 && r < len) d[i] = rec[r];
+        for (int u = 0; u < kCompactUnroll; u++) {
+            const int64_t j = jb + u * kWave + tid;
+            const int64_t g = j - gshift;
+            A[u] = u32x4{0u, 0u, 0u, 0u};
+            Bv[u] = u32x4{0u, 0u, 0u, 0u};
+            if (j < nq) {
+                if (g >= 0) A[u] = rec16[g];
+                if (m) Bv[u] = rec16[g + 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCompactUnroll; u++) {
+            const int64_t j = jb + u * kWave + tid;
+            if (j >= nq) continue;
+            const int64_t s = 16 * j - m;
+            const u32x4 v = pair_bytes(A[u], Bv[u], t);
+            gbl8* d = d0 + 16 * j;
+            if (s >= 0 && s + 16 <= len) {
+                *(gbl128*)d = v;
+            } else {
+                const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if (s + i >= 0 && s + i < len) d[i] = (uint8_t)(vw[i >> 2] >> (8 * (i & 3)));
             }
         }
     }
