@@ -16,7 +16,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add((f, r["Dispatch_Id"]))
 for k, v in acc.items():
-    if not any(x in k for x in ("encode", "decode", "idx", "compact")):
+    if not any(x in k for x in ("encode", "decode", "idx", "compact", "scan")):
         continue
     print("==", k, "dispatches", len(disp[k]))
     for c in sorted(v):

@@ -1,5 +1,8 @@
-"""Run one device-resident compress (+ optionally decompress) of G1 data, for
-profilers.  Usage: python tools/run_codec_once.py [GiB] [enc|dec|both]"""
+"""Run one device-resident compress (+ optionally decompress) of synthetic
+data, for profilers.  Usage:
+    python tools/run_codec_once.py [GiB] [enc|dec|both] [gen]
+gen 1 (default) = int16 G1 (config 2's data, seed 12345), 2 = float32 G2
+(config 3's data)."""
 import os
 import sys
 
@@ -11,12 +14,14 @@ from bitshuffle_amd import api  # noqa: E402
 
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
 what = sys.argv[2] if len(sys.argv) > 2 else "both"
-n = int(gib * (1 << 30)) // 2
-x = torch.empty(n, dtype=torch.int16, device="cuda")
-B.synth_fill_dev(x, 1)
+gen = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+dt = torch.int16 if gen == 1 else torch.float32
+n = int(gib * (1 << 30)) // torch.empty(0, dtype=dt).element_size()
+x = torch.empty(n, dtype=dt, device="cuda")
+B.synth_fill_dev(x, gen)
 c = api.compress_lz4_dev(x)
 if what in ("dec", "both"):
     y = api.decompress_lz4_dev(c, x.shape, x.dtype)
-    assert torch.equal(x, y)
+    assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
 torch.cuda.synchronize()
 print("ok", c.numel())
