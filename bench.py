@@ -168,6 +168,25 @@ def load_pmc_traffic():
         return None
 
 
+def copy_peak_gbps(dev, nbytes=2 << 30, reps=5):
+    """Achievable HBM bandwidth on this box: a device-to-device
+    copy of nbytes, timed with events on torch's current stream, read + write
+    bytes per second.  Outside the timed region."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e.record()
+    e.synchronize()
+    gbps = 2.0 * nbytes * reps / (s.elapsed_time(e) / 1e3) / 1e9
+    del a, b
+    return gbps
+
+
 # ---------------------------------------------------------------- CPU baseline
 def cpu_model():
     try:
@@ -384,6 +403,13 @@ def main(argv=None):
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "alg_bytes_per_launch": alg.get(dom, nbytes + C),
                     "avg_launch_ms": round(avg_s * 1e3, 4)}
+        try:
+            cp = copy_peak_gbps(dev)
+            roofline["achievable_copy_GBps"] = round(cp, 1)
+            roofline["frac_of_achievable"] = round(ach / cp, 4)
+        except Exception as e:  # reported, never fatal for the line
+            roofline["achievable_copy_GBps"] = None
+            roofline["copy_error"] = repr(e)
     # whole round trip priced as SURVEY.md 8(d): 2(N+C) algorithmic bytes per
     # GPU for the codec, 4N for a transpose round trip
     per_step = 4.0 * nbytes if cfg["what"] == "shuffle" else 2.0 * (nbytes + C)

@@ -8,9 +8,10 @@
  *      and its inverse bshuf_untrans_bit_elem_scal, :369-387);
  *   - the greedy LZ4 v1.10.0 block parse exactly as LZ4_compress_default runs
  *     it for a fresh, zeroed state (lz4/lz4.c:930-1338, 1382-1403, 1472);
- *   - a bounds-checked LZ4 block decoder (semantics of LZ4_decompress_safe,
- *     lz4/lz4.c:2451; error *values* on malformed input are not reproduced,
- *     only their sign);
+ *   - a bounds-checked LZ4 block decoder restating LZ4_decompress_safe's fast
+ *     and safe loops (lz4/lz4.c:2022-2445, 2451), so malformed input gets the
+ *     reference's accept/reject decision, error value -(pos)-1 and output
+ *     (pinned against the compiled reference in tests/test_oracle.py);
  *   - bitshuffle's framing: per block u32 big-endian length + LZ4 payload,
  *     partial last block, n%8 raw tail (src/bitshuffle.c:36-119,
  *     src/bitshuffle_core.c:1877-1931).
