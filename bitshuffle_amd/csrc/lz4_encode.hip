@@ -151,43 +151,43 @@ constexpr int kWinBytes = 4 * kWave;  // bytes one dword-per-lane wave access co
 
 // ---------------------------------------------------------------------------
 // Emission policies of the parse.  The parse reports each sequence once its
-// match is final (seq) and the trailing literal run (last); `op` is the
-// running compressed size, kept by the parse in SGPRs.
+// match is final (seq) and the trailing literal run (last).
 //
-//  * EmitDesc (default): the lane-0 store of an 8-byte descriptor into LDS;
-//    the LZ4 bytes are built afterwards by emit_sequences, wave-parallel, so
-//    literal copies and length runs are off the serial parse entirely.
+//  * EmitDesc (default): an 8-byte descriptor per sequence in LDS; the LZ4
+//    bytes (and the record size) come afterwards from emit_sequences,
+//    wave-parallel, so literal copies, length runs and size bookkeeping are
+//    off the serial parse entirely.
 //  * EmitBytes: writes the bytes straight to global memory from inside the
-//    parse (blocks whose record does not fit the LDS staging area, the rare
-//    block with more sequences than descriptor slots, and the A/B variant 2).
+//    parse, `op` being the running compressed size (blocks whose record does
+//    not fit the LDS staging area, the rare block with more sequences than
+//    descriptor slots, and the A/B variant 2).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int seq_bytes(int lit, int mc) {
-    return 3 + lz4_ext_bytes(lit) + lit + lz4_ext_bytes(mc);
-}
 
 constexpr int kDescMax = 256;              // descriptor slots per block
 constexpr int kDescBytes = 8 * kDescMax;   // LDS behind the block
 
+// Sequence s's descriptor: two dwords in LDS (ip | off << 16, lit | mc << 16),
+// stored by lane 0.  The record size is not tracked during the parse:
+// emit_sequences' prefix sum gives it.
 struct EmitDesc {
-    lds32* desc;  // 2 dwords per sequence: ip | off << 16, lit | mc << 16
+    lds32* desc;
     int lane;
     int ns = 0;   // sequences recorded
     int la = 0;   // anchor of the last literal run
     __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
         if (ns >= kDescMax) return false;
-        const int lit = ip - anchor;
         if (lane == 0) {
             ((lds64v*)desc)[ns] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
-                                        (uint32_t)lit | ((uint32_t)mc << 16)};
+                                        (uint32_t)(ip - anchor) | ((uint32_t)mc << 16)};
         }
         ns++;
-        op += seq_bytes(lit, mc);
+        (void)op;
         return true;
     }
     __device__ __forceinline__ void last(int& op, int anchor, int n) {
+        (void)op;
+        (void)n;
         la = anchor;
-        const int run = n - anchor;
-        op += 1 + lz4_ext_bytes(run) + run;
     }
 };
 
@@ -251,8 +251,10 @@ struct EmitBytes {
 // Builds the LZ4 bytes of a parsed block from its descriptors, wave-parallel
 // (lane = sequence; a prefix sum places every sequence): record payload at
 // S[4..), literals from the block D.  The last literal run is sequence ns.
-__device__ __forceinline__ void emit_sequences(const lds8* D, const lds32* desc, const int ns, const int la,
-                               const int n, lds8* S, const int lane) {
+// Returns the payload size.
+__device__ __forceinline__ int emit_sequences(const lds8* D, const EmitDesc& em, const int n, lds8* S,
+                                              const int lane) {
+    const int ns = em.ns, la = em.la;
     int opb = 4;
     for (int b0 = 0; b0 <= ns; b0 += kWave) {
         const int s = b0 + lane;
@@ -260,11 +262,12 @@ __device__ __forceinline__ void emit_sequences(const lds8* D, const lds32* desc,
         const bool act = s <= ns;
         int ip = n, off = 0, lit = act ? n - la : 0, mc = 0;
         if (m) {
-            const u32x2 d = ((const lds64v*)desc)[s];
-            ip = (int)(d.x & 0xFFFFu);
-            off = (int)(d.x >> 16);
-            lit = (int)(d.y & 0xFFFFu);
-            mc = (int)(d.y >> 16);
+            const u32x2 d = ((const lds64v*)em.desc)[s];
+            const uint32_t x = d.x, y = d.y;
+            ip = (int)(x & 0xFFFFu);
+            off = (int)(x >> 16);
+            lit = (int)(y & 0xFFFFu);
+            mc = (int)(y >> 16);
         }
         const int le = lz4_ext_bytes(lit), me = m ? lz4_ext_bytes(mc) : 0;
         const int len = act ? 1 + le + lit + (m ? 2 + me : 0) : 0;
@@ -286,6 +289,7 @@ __device__ __forceinline__ void emit_sequences(const lds8* D, const lds32* desc,
         }
         lane_len_run(S, lp + lit + 2, me, (uint32_t)(mc - 15) % 255u);
     }
+    return opb - 4;
 }
 
 // Catch-up (lz4/lz4.c:1105-1109) and LZ4_count (lz4/lz4.c:680-703) in one
@@ -380,6 +384,22 @@ __device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip
     }
 }
 
+// One lane's probe of the search skip schedule, advanced one window (64
+// probes) at a time: with t = 62 + k, q = t >> 6 grows by one per window while
+// t & 63 stays, so the closed form of probe_offset (exact for k >= 1; it gives
+// 1 for k = 0) moves by 64 q + (t & 63) + 1, and that step by 64.
+struct ProbeLane {
+    int off, step;
+    __device__ __forceinline__ void advance() {
+        off += step;
+        step += kWave;
+    }
+};
+__device__ __forceinline__ ProbeLane probe_lane(int k) {
+    const int t = 62 + k, q = t >> 6, r = t & 63;
+    return ProbeLane{1 + 32 * q * (q - 1) + q * (r + 1), 64 * q + r + 1};
+}
+
 // read32 at position p from the a-side window registers (p - base in
 // [0, 252]), without an LDS round trip.
 __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
@@ -387,7 +407,8 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
     const int l = t >> 2;
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, min(l + 1, kWave - 1));
-    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(t & 3));
+    // a 64-bit scalar shift keeps the value (and its hash) in SGPRs
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (t & 3)));
 }
 
 // Greedy LZ4 parse of D[0..n) with table T (zeroed).  Every sequence goes to
@@ -413,14 +434,21 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                 const int p0 = ip;
                 COUNT(6, 1);
                 uint32_t seq_cur = pre;  // valid for k0 == 0 (positions p0 + lane)
+                // probe offsets by addition: this lane's probe k and probe k+1
+                // (the closed form's value, which is 1 for k = 0: `bias`)
+                ProbeLane q0 = probe_lane(lane), q1 = probe_lane(lane + 1);
+                int bias = lane == 0 ? 1 : 0;
                 for (int k0 = 0;; k0 += kWave) {
                     COUNT(1, 1);
-                    const int pos = p0 + probe_offset(k0 + lane);
-                    const bool valid = p0 + probe_offset(k0 + lane + 1) <= limit;
+                    const int pos = p0 + q0.off - bias;
+                    const bool valid = p0 + q1.off <= limit;
                     const uint64_t vmask = ballot(valid);
                     if (vmask == 0) break;
                     // next window's sequences, in flight while this one resolves
-                    const int pos_n = p0 + probe_offset(k0 + kWave + lane);
+                    const int pos_n = p0 + q0.off + q0.step;
+                    q0.advance();
+                    q1.advance();
+                    bias = 0;
                     const uint32_t seq_nxt = lds_rd32(D, min(pos_n, n));
                     const uint32_t seq = seq_cur;
                     if constexpr (!READBACK) {
@@ -444,7 +472,7 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                         const uint64_t mm = ballot(ok);
                         if (mm) {
                             const int js = ffs64(mm);
-                            mpos = p0 + probe_offset(k0 + js);
+                            mpos = __builtin_amdgcn_readlane(pos, js);
                             // positions after the match were never inserted: the
                             // first later lane of each entry puts back what it found
                             // (found <= mpos: no lane between wrote that entry)
@@ -776,14 +804,13 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         constexpr bool kDesc = !WIDE && (VAR & 2) == 0;
         if constexpr (kDesc) {
             if (a.desc_ok && 4 + lz4_bound(n) + 15 <= kTableBytes) {
-                lds32* desc = (lds32*)(D + a.desc_off);
-                EmitDesc em{desc, lane};
+                EmitDesc em{(lds32*)(D + a.desc_off), lane};
                 c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     lds8* S = to_lds(smem);
-                    emit_sequences(D, desc, em.ns, em.la, n, S, lane);
+                    c = emit_sequences(D, em, n, S, lane);
                     if (lane < 4) S[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();

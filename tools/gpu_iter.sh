@@ -12,8 +12,9 @@ KARG=()
 [ -n "$K" ] && KARG=(-k "$K")
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider "${KARG[@]}" > gpurun_out/${TAG}_pytest.log 2>&1 && \
 timeout -k 10 300 python -u tools/ab.py $AB 2 1 3 > gpurun_out/${TAG}_ab.log 2>&1 && \
+timeout -k 10 300 python -u tools/ab.py $AB 2 2 2 > gpurun_out/${TAG}_ab_g2.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?
 tail -4 gpurun_out/${TAG}_pytest.log
-cat gpurun_out/${TAG}_ab.log gpurun_out/${TAG}_bench.json 2>/dev/null
+cat gpurun_out/${TAG}_ab.log gpurun_out/${TAG}_ab_g2.log gpurun_out/${TAG}_bench.json 2>/dev/null
 exit $rc
