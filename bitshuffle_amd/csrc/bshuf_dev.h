@@ -40,7 +40,9 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// the wave64 ballot of a condition straight from its compare (no 0/1
+// materialisation and re-compare, as __ballot(int) compiles to)
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
 __device__ __forceinline__ int fls64(uint64_t m) { return 63 - __clzll((long long)m); }
 

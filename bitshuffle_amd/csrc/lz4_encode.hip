@@ -85,9 +85,14 @@ struct EncArgs {
 
 // Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
 // asm waits for its own result, so the compiler never reads it early.
-__device__ __forceinline__ uint32_t lds_addr(void* p) {
-    return (uint32_t)(uintptr_t)(lds8*)p;
-}
+__device__ __forceinline__ uint32_t lds_addr(lds8* p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ uint32_t lds_addr(void* p) { return (uint32_t)(uintptr_t)(lds8*)p; }
+
+// k_lz4_encode has no static LDS, so its dynamic LDS starts at address 0
+// (checked on the host before the launch, lds_layout_ok).  Addressing it from
+// the constant 0 instead of the extern array's relocated address lets the
+// compiler fold constant offsets into the DS instructions' immediates.
+__device__ __forceinline__ lds8* lds_origin() { return (lds8*)(uintptr_t)0; }
 __device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t addr, uint32_t mask, uint32_t data) {
     uint32_t r;
     asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
@@ -110,7 +115,7 @@ typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 
 template <bool WIDE>
 struct Table {
-    uint8_t* base;
+    lds8* base;
     __device__ __forceinline__ uint32_t get(uint32_t h) const {
         if constexpr (WIDE)
             return ((lds_vu32*)base)[h];
@@ -464,12 +469,10 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                             cand = T.exchange(h, (uint32_t)pos);
                         }
                         const uint32_t dcand = lds_rd32(D, (int)cand);
-                        bool ok = false;
-                        if (valid) {
-                            const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
-                            ok = near && dcand == seq;
-                        }
-                        const uint64_t mm = ballot(ok);
+                        // the compare's own mask, and-ed with the valid lanes on the
+                        // scalar unit (a ballot of a combined bool is materialised)
+                        const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
+                        const uint64_t mm = vmask & ballot(WIDE ? (near & (dcand == seq)) : dcand == seq);
                         if (mm) {
                             const int js = ffs64(mm);
                             mpos = __builtin_amdgcn_readlane(pos, js);
@@ -520,12 +523,10 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                         // candidate bytes: the table's position, or the in-window predecessor's
                         const uint32_t dpred = (uint32_t)__shfl((int)seq, pred < 0 ? lane : pred);
                         const uint32_t dcand = pred < 0 ? dcold : dpred;
-                        bool ok = false;
-                        if (valid) {
-                            const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
-                            ok = near && dcand == seq;
-                        }
-                        const uint64_t mm = ballot(ok);
+                        // the compare's own mask, and-ed with the valid lanes on the
+                        // scalar unit (a ballot of a combined bool is materialised)
+                        const bool near = !WIDE || cand + kMaxDistance >= (uint32_t)pos;
+                        const uint64_t mm = vmask & ballot(WIDE ? (near & (dcand == seq)) : dcand == seq);
                         if (mm) {
                             const int js = ffs64(mm);
                             if (valid) {
@@ -708,7 +709,9 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
     const int E = EK ? EK : a.L.E;
-    lds8* D = to_lds(smem) + kTableBytes;
+    (void)smem;
+    lds8* const L0 = lds_origin();
+    lds8* D = L0 + kTableBytes;
     const int64_t stride = gridDim.x;
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
@@ -751,7 +754,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         const uint8_t* src = blk_src(blk);
         // zero the hash table (LZ4_initStream) and the read pad behind the block
         for (int i = lane; i < kTableBytes / 16; i += kWave)
-            ((lds128*)to_lds(smem))[i] = u32x4{0u, 0u, 0u, 0u};
+            ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
         if (lane < kDataPad / 4) ((lds32*)(D + ((n + 3) & ~3)))[lane] = 0;
         // bit transpose into LDS (bshuf_trans_bit_elem)
         if constexpr (EK != 0) {
@@ -797,7 +800,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         }
 
         uint8_t* out = a.scratch + blk * a.slot;
-        const Table<WIDE> T{smem};
+        const Table<WIDE> T{L0};
         int c = -1;
         // default: descriptors during the parse, bytes afterwards (the record
         // is staged in the table's LDS, dead once the parse is over)
@@ -809,7 +812,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
-                    lds8* S = to_lds(smem);
+                    lds8* S = L0;
                     c = emit_sequences(D, em, n, S, lane);
                     if (lane < 4) S[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -821,7 +824,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                     // more sequences than descriptor slots: parse again with
                     // the inline emitter (fresh table)
                     for (int i = lane; i < kTableBytes / 16; i += kWave)
-                        ((lds128*)to_lds(smem))[i] = u32x4{0u, 0u, 0u, 0u};
+                        ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 }
@@ -1025,6 +1028,13 @@ bool lds_atomics_lane_ordered() {
     return ordered;
 }
 
+// The encoder addresses its dynamic LDS from address 0 (lds_origin): true
+// when the kernel has no static LDS in front of it.
+bool lds_layout_ok(const void* fn) {
+    hipFuncAttributes at{};
+    return hipFuncGetAttributes(&at, fn) == hipSuccess && at.sharedSizeBytes == 0;
+}
+
 template <int EK, bool WIDE, int VAR = 0>
 hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s) {
     if constexpr (EK == 2 && !WIDE && VAR == 0) {
@@ -1039,6 +1049,7 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
     }
     auto fn = k_lz4_encode<EK, WIDE, VAR>;
+    if (!lds_layout_ok(reinterpret_cast<const void*>(fn))) return hipErrorInvalidDeviceFunction;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
