@@ -313,11 +313,11 @@ struct CountOut {
 // equal bytes from ip itself (the first window's lane 0 is the 4-byte
 // test).  cnt = match length beyond kMinMatch, or -1 when there is no match.
 __device__ __forceinline__ CountOut test_and_count(const lds8* D, int n, int ip, int ref,
-                                                   int mlimit, int lane) {
+                                                   int mlimit, int lane, uint32_t va0) {
     CountOut r;
     r.back = 0;
     int pa = ip + 4 * lane, pb = ref + 4 * lane;
-    uint32_t va = lds_rd32(D, min(pa, n)), vb = lds_rd32(D, min(pb, n));
+    uint32_t va = va0, vb = lds_rd32(D, min(pb, n));  // va0: the a-side, read ahead
     if (__builtin_amdgcn_readfirstlane(va ^ vb) != 0) {
         r.cnt = -1;
         return r;
@@ -412,8 +412,7 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
     const int l = t >> 2;
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, min(l + 1, kWave - 1));
-    // a 64-bit scalar shift keeps the value (and its hash) in SGPRs
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (t & 3)));
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(t & 3));
 }
 
 // Greedy LZ4 parse of D[0..n) with table T (zeroed).  Every sequence goes to
@@ -579,8 +578,10 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                     h2 = hash_at<WIDE>(D, ip - 2);
                     h0 = hash_at<WIDE>(D, ip);
                 }
-                // the next search window's bytes, in flight during the re-test
+                // the next search window's bytes and the test's a-side window,
+                // in flight during the table exchange
                 pre = lds_rd32(D, min(ip + 1 + lane, n));
+                const uint32_t va0 = lds_rd32(D, min(ip + 4 * lane, n));
                 uint32_t c2 = 0;
                 if (lane == 0) {
                     T.put(h2, (uint32_t)(ip - 2));
@@ -589,7 +590,7 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                 c2 = uni(c2);
                 const bool near = !WIDE || c2 + kMaxDistance >= (uint32_t)ip;
                 if (near) {
-                    co = test_and_count(D, n, ip, (int)c2, mlimit, lane);
+                    co = test_and_count(D, n, ip, (int)c2, mlimit, lane, va0);
                     if (co.cnt >= 0) {
                         // zero-literal sequence, no catch-up on this path
                         ref = (int)c2;
