@@ -7,17 +7,47 @@
 
 namespace bshuf {
 
+// mem[addr] = (mem[addr] & ~mask) | data: a masked dword write in one DS
+// instruction (non-returning ds_mskor_b32; data must be zero outside mask).
+// Same-address lanes of one instruction are applied one after another, so
+// neighbours sharing a dword both land.
+__device__ __forceinline__ void lds_write_masked(uint32_t addr, uint32_t mask, uint32_t data) {
+    asm volatile("ds_mskor_b32 %0, %1, %2" : : "v"(addr), "v"(mask), "v"(data) : "memory");
+}
+
+// The low r bytes of a dword set (r clamped to [0, 4]).
+__device__ __forceinline__ uint32_t low_bytes_mask(int r) {
+    r = min(r, 4);
+    return r <= 0 ? 0u : 0xFFFFFFFFu >> (32 - 8 * r);
+}
+
 // One lane copies n <= 16 bytes (from a buffer with >= 16 readable bytes past
-// sp, or whose over-read stays inside LDS and is discarded).
+// sp, or whose over-read stays inside LDS and is discarded).  The source's 16
+// bytes come from five dword reads and v_alignbyte; the <= 5 destination
+// dwords they touch are each written by one masked write (v_perm shifts the
+// bytes into place), so there are no per-byte branches.  Every read is issued
+// before any write, so a lane may copy from bytes other lanes overwrite.
 __device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int dp, int n) {
     const lds32* w = (const lds32*)(S + (sp & ~3));
     const uint32_t sh = (uint32_t)(sp & 3);
     const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-    const uint32_t v[4] = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
-                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+    const uint32_t u[6] = {0u,
+                           __builtin_amdgcn_alignbyte(x1, x0, sh),
+                           __builtin_amdgcn_alignbyte(x2, x1, sh),
+                           __builtin_amdgcn_alignbyte(x3, x2, sh),
+                           __builtin_amdgcn_alignbyte(x4, x3, sh),
+                           0u};
+    // destination dword j holds source bytes 4j - k .. 4j - k + 3
+    const int k = dp & 3, e = k + n;
+    const uint32_t sel = 0x03020100u + (uint32_t)(4 - k) * 0x01010101u;
+    const uint32_t base = (uint32_t)(uintptr_t)(Dd + (dp & ~3));
 #pragma unroll
-    for (int i = 0; i < 16; i++)
-        if (i < n) Dd[dp + i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+    for (int j = 0; j < 5; j++) {
+        uint32_t m = low_bytes_mask(e - 4 * j);
+        if (j == 0) m &= ~low_bytes_mask(k);
+        const uint32_t d = __builtin_amdgcn_perm(u[j + 1], u[j], sel) & m;
+        lds_write_masked(base + 4u * (uint32_t)j, m, d);
+    }
 }
 
 // The whole wave copies n bytes whose source ends at or before the

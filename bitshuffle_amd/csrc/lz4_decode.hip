@@ -894,7 +894,14 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
             if (diag_variant() == 72) fn = BSHUF_DEC(2, 72);
 #endif
             break;
-        case 4: fn = BSHUF_DEC(4, 0); break;
+        case 4:
+            fn = BSHUF_DEC(4, 0);
+#ifdef BSHUF_DIAG
+            if (diag_variant() == 8) fn = BSHUF_DEC(4, 8);
+            if (diag_variant() == 64) fn = BSHUF_DEC(4, 64);
+            if (diag_variant() == 72) fn = BSHUF_DEC(4, 72);
+#endif
+            break;
         case 8: fn = BSHUF_DEC(8, 0); break;
         default: fn = BSHUF_DEC(0, 0); break;
     }
