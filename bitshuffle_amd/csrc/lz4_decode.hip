@@ -276,8 +276,20 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
     }
     const int s = mop - off;
     const float rinv = 1.0f / (float)off;
+    if (ml <= kWave) {
+        // i mod off for i < 64, off < 64: q = (i * inv) >> 16 with inv in
+        // [2^16 / off, 2^16 / off + 2) is exact (its error i * 2 / 2^16 < 1/512
+        // stays below the gap 1/off to the next integer), on full-rate 24-bit
+        // multiplies
+        const uint32_t inv = (uint32_t)(65536.0f * rinv) + 1u;
+        if (lane < ml) {
+            const uint32_t q = __umul24((uint32_t)lane, inv) >> 16;
+            D[mop + lane] = D[s + lane - (int)__umul24(q, (uint32_t)off)];
+        }
+        return;
+    }
     const int q0 = (mop + 3) & ~3, q1 = (mop + ml) & ~3;
-    if (q1 <= q0 || ml <= kWave) {
+    if (q1 <= q0) {
         for (int i = lane; i < ml; i += kWave) D[mop + i] = D[s + small_mod(i, off, rinv)];
         return;
     }
