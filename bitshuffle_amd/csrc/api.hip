@@ -625,6 +625,17 @@ bool stage_init(HostCtx& c) {
 
 // Appends `n` bytes host -> device at dst (piece by piece; returns at once
 // after the last memcpy, the DMA may still run).
+// Before a device->host copy of results: every XCD's L2 written back to
+// memory (a system-scope release per workgroup; 256 workgroups reach all 8
+// XCDs).  Without it the copy was seen to read stale bytes of lines the
+// stream's last kernel had just written (finish_visible, bshuf_dev.h).
+__global__ __launch_bounds__(64) void k_host_release() { __threadfence_system(); }
+
+hipError_t host_visible(hipStream_t s) {
+    hipLaunchKernelGGL(k_host_release, dim3(256), dim3(64), 0, s);
+    return hipGetLastError();
+}
+
 hipError_t h2d(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s) {
     HostCtx& c = host_ctx();
     if (!(staging_mode() & 1) || !stage_init(c)) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
@@ -691,7 +702,8 @@ static int64_t transpose_host(const void* in, void* out, size_t size, size_t ele
     if (h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) return kErrHip;
     const int64_t n = transpose_dev(di, dout, size, elem_size, block_size, s, fwd);
     if (n < 0) return n;
-    if (d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess) return kErrHip;
+    if (host_visible(s) != hipSuccess || d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess)
+        return kErrHip;
     return n;
 }
 
@@ -725,7 +737,8 @@ int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const s
                                              nullptr, s);
     if (e < 0) return e;
     int64_t res = 0;
-    if (hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (host_visible(s) != hipSuccess ||
+        hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return kErrHip;
     if (res > 0 && (size_t)res <= bound &&
@@ -792,7 +805,8 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const
                                                nullptr, 0, dres, doffs, s);
     if (e < 0) return e;
     int64_t res = 0;
-    if (hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (host_visible(s) != hipSuccess ||
+        hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return kErrHip;
     if (res >= 0 && bytes && d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess)

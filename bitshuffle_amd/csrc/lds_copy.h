@@ -21,16 +21,10 @@ __device__ __forceinline__ uint32_t low_bytes_mask(int r) {
     return r <= 0 ? 0u : 0xFFFFFFFFu >> (32 - 8 * r);
 }
 
-// One lane copies n <= 16 bytes (from a buffer with >= 16 readable bytes past
-// sp, or whose over-read stays inside LDS and is discarded).  The source's 16
-// bytes come from five dword reads and v_alignbyte; the <= 5 destination
-// dwords they touch are each written by one masked write (v_perm shifts the
-// bytes into place), so there are no per-byte branches.  Every read is issued
-// before any write, so a lane may copy from bytes other lanes overwrite.
-__device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int dp, int n) {
-    const lds32* w = (const lds32*)(S + (sp & ~3));
-    const uint32_t sh = (uint32_t)(sp & 3);
-    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+// The destination half of lane_copy16: x0..x4 are the five source dwords
+// around the first source byte, sh its offset in x0.
+__device__ __forceinline__ void lane_put16(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3,
+                                           uint32_t x4, uint32_t sh, lds8* Dd, int dp, int n) {
     const uint32_t u[6] = {0u,
                            __builtin_amdgcn_alignbyte(x1, x0, sh),
                            __builtin_amdgcn_alignbyte(x2, x1, sh),
@@ -48,6 +42,17 @@ __device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int
         const uint32_t d = __builtin_amdgcn_perm(u[j + 1], u[j], sel) & m;
         lds_write_masked(base + 4u * (uint32_t)j, m, d);
     }
+}
+
+// One lane copies n <= 16 bytes (from a buffer with >= 16 readable bytes past
+// sp, or whose over-read stays inside LDS and is discarded).  The source's 16
+// bytes come from five dword reads and v_alignbyte; the <= 5 destination
+// dwords they touch are each written by one masked write (v_perm shifts the
+// bytes into place), so there are no per-byte branches.  Every read is issued
+// before any write, so a lane may copy from bytes other lanes overwrite.
+__device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int dp, int n) {
+    const lds32* w = (const lds32*)(S + (sp & ~3));
+    lane_put16(w[0], w[1], w[2], w[3], w[4], (uint32_t)(sp & 3), Dd, dp, n);
 }
 
 // The whole wave copies n bytes whose source ends at or before the

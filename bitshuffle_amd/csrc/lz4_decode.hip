@@ -23,6 +23,8 @@
 // expected number of blocks is rejected.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "launch.h"
 #include "lds_copy.h"
 #include "lz4_scan.h"
@@ -316,9 +318,68 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
     }
 }
 
+// Where phase 2 reads a record from.  LdsRec: the record staged in LDS (byte
+// p at C[p]).  GblRec (VAR & 16): straight from the stream in HBM / L2, byte p
+// at base + p, so the LDS holds only the decoded block (twice the resident
+// waves).  Reads are absolute-aligned dwords clamped to the last dword holding
+// a payload byte, so an over-read never leaves the record's pages; the bytes
+// past the payload it returns are never used (the scan validated every field).
+struct LdsRec {
+    const lds8* C;
+    __device__ __forceinline__ uint64_t rd64(int p) const { return lds_rd64(C, p); }
+    __device__ __forceinline__ void copy16(int sp, lds8* D, int dp, int n) const {
+        lane_copy16(C, sp, D, dp, n);
+    }
+    __device__ __forceinline__ void copyw(int sp, lds8* D, int dp, int n, int lane) const {
+        wave_copy(C, sp, D, dp, n, lane);
+    }
+};
+
+typedef __attribute__((address_space(1))) const uint32_t gbl32c;
+typedef __attribute__((address_space(1))) const uint8_t gbl8c;
+
+struct GblRec {
+    uintptr_t base;   // absolute address of payload byte 0
+    uintptr_t lastw;  // the last aligned dword holding a payload byte
+    __device__ __forceinline__ uint32_t w(uintptr_t a) const {
+        return *(gbl32c*)(a < lastw ? a : lastw);
+    }
+    __device__ __forceinline__ uint64_t rd64(int p) const {
+        const uintptr_t a = base + (uintptr_t)p, al = a & ~(uintptr_t)3;
+        const uint32_t s = (uint32_t)(a & 3);
+        const uint32_t w0 = w(al), w1 = w(al + 4), w2 = w(al + 8);
+        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, s) |
+               ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32);
+    }
+    __device__ __forceinline__ void copy16(int sp, lds8* D, int dp, int n) const {
+        const uintptr_t a = base + (uintptr_t)sp, al = a & ~(uintptr_t)3;
+        lane_put16(w(al), w(al + 4), w(al + 8), w(al + 12), w(al + 16), (uint32_t)(a & 3), D, dp, n);
+    }
+    __device__ __forceinline__ void copyw(int sp, lds8* D, int dp, int n, int lane) const {
+        const gbl8c* S = (const gbl8c*)(base + (uintptr_t)sp);
+        if (n <= kWave) {
+            if (lane < n) D[dp + lane] = S[lane];
+            return;
+        }
+        const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
+        const int head = q0 - dp, tailn = dp + n - q1;
+        const int e = lane < 4 ? lane : n - tailn + (lane - 4);
+        if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn)) D[dp + e] = S[e];
+        const int nw = (q1 - q0) >> 2;
+        const uintptr_t a0 = base + (uintptr_t)(sp + head);
+        const uint32_t sh = (uint32_t)(a0 & 3);
+        const uintptr_t al0 = a0 & ~(uintptr_t)3;
+        for (int c = lane; c < nw; c += kWave) {
+            const uintptr_t al = al0 + 4 * (uintptr_t)c;
+            ((lds32*)(D + q0))[c] = __builtin_amdgcn_alignbyte(w(al + 4), w(al), sh);
+        }
+    }
+};
+
 // LZ4 length continuation starting at record byte q, whose next `av` bytes
 // (av <= 8) are already in w: returns the added length, advances q.
-__device__ __forceinline__ int read_ext(const lds8* Cb, int& q, uint64_t w, int av) {
+template <class Src>
+__device__ __forceinline__ int read_ext(const Src& Cb, int& q, uint64_t w, int av) {
     int v = 0;
     for (;;) {
         uint64_t inv = ~w;
@@ -330,7 +391,7 @@ __device__ __forceinline__ int read_ext(const lds8* Cb, int& q, uint64_t w, int 
         }
         v += 255 * av;
         q += av;
-        w = lds_rd64(Cb, q);
+        w = Cb.rd64(q);
         av = 8;
     }
 }
@@ -338,7 +399,8 @@ __device__ __forceinline__ int read_ext(const lds8* Cb, int& q, uint64_t w, int 
 // Phase 2 for one block.  The record payload starts at byte cp of the
 // 4-aligned LDS buffer Cb; pos[0..nseq) are its token positions (payload-
 // relative, validated by the scan); pos0 is this lane's prefetched pos[lane].
-__device__ __forceinline__ void lz4_exec_block(const lds8* Cb, const int cp, lds8* D,
+template <class Src>
+__device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8* D,
                                const uint32_t* __restrict__ pos, const int nseq, uint32_t pos0,
                                const int lane) {
     int opb = 0;
@@ -352,7 +414,7 @@ __device__ __forceinline__ void lz4_exec_block(const lds8* Cb, const int cp, lds
         // behind it in one read (a zero-literal sequence's offset and first
         // length bytes are among them), else one more read at the offset
         const int p = cp + tp;
-        const uint64_t x = lds_rd64(Cb, p);
+        const uint64_t x = Cb.rd64(p);
         const int tok = (int)(x & 255u);
         int lit = act ? tok >> 4 : 0;
         int q = p + 1;
@@ -362,7 +424,7 @@ __device__ __forceinline__ void lz4_exec_block(const lds8* Cb, const int cp, lds
         int off = 0, ml = 0;
         if (act && j + 1 < nseq) {  // the last sequence has no match
             const int d = q - p;    // bytes of x already behind q
-            const uint64_t y = d <= 6 ? x >> (8 * d) : lds_rd64(Cb, q);
+            const uint64_t y = d <= 6 ? x >> (8 * d) : Cb.rd64(q);
             const int yav = d <= 6 ? 8 - d : 8;
             off = (int)(y & 0xFFFFu);
             q += 2;
@@ -375,11 +437,11 @@ __device__ __forceinline__ void lz4_exec_block(const lds8* Cb, const int cp, lds
         const int op = opb + incl - len;
         opb += __builtin_amdgcn_readlane(incl, kWave - 1);
         // ---- literals: short runs per lane, long runs by the whole wave
-        if (lit > 0 && lit <= 16) lane_copy16(Cb, lsrc, D, op, lit);
+        if (lit > 0 && lit <= 16) Cb.copy16(lsrc, D, op, lit);
         for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
             const int l = ffs64(lm);
-            wave_copy(Cb, __builtin_amdgcn_readlane(lsrc, l), D, __builtin_amdgcn_readlane(op, l),
-                      __builtin_amdgcn_readlane(lit, l), lane);
+            Cb.copyw(__builtin_amdgcn_readlane(lsrc, l), D, __builtin_amdgcn_readlane(op, l),
+                     __builtin_amdgcn_readlane(lit, l), lane);
         }
         // ---- matches, in batches of mutually independent sequences
         const int mop = op + lit;
@@ -652,6 +714,8 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     const int E = EK ? EK : a.L.E;
     lds8* D = to_lds(smem);             // decoded (bit-shuffled) block
     lds8* Cbuf = to_lds(smem) + a.cap + 16;  // record bytes, 16-aligned base
+    // VAR & 16: phase 2 reads the record from global memory (no LDS copy)
+    constexpr bool kG = (VAR & 16) != 0;
     const int64_t stride = gridDim.x;
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
@@ -659,7 +723,9 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     PayRegs R;
     Span cur = span_from(a, issue_offs(a, blk, nb, lane), nb);
     uint32_t cur_pos;
-    {
+    if constexpr (kG) {
+        cur_pos = cur.loc.seq[cur.o0 / 3 + lane];
+    } else {
         const bool in_regs = span_fits(a, cur);
         if (in_regs) issue_pay(R, a, cur, lane);
         cur_pos = land_record(R, in_regs, a, cur, Cbuf, lane);
@@ -667,10 +733,15 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     int64_t next = blk + stride;
     Span nxt = {};
     bool nxt_in_regs = false;
+    uint32_t pref_pos = 0;  // kG: token position of block `next`, loaded a parse early
     if (next < nb) {
         nxt = span_from(a, issue_offs(a, next, nb, lane), nb);
-        nxt_in_regs = span_fits(a, nxt);
-        if (nxt_in_regs) issue_pay(R, a, nxt, lane);
+        if constexpr (kG) {
+            pref_pos = nxt.loc.seq[nxt.o0 / 3 + lane];
+        } else {
+            nxt_in_regs = span_fits(a, nxt);
+            if (nxt_in_regs) issue_pay(R, a, nxt, lane);
+        }
     }
     OffRegs O{0, 0};
     if (next + stride < nb) O = issue_offs(a, next + stride, nb, lane);
@@ -685,10 +756,18 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         int status = 0, clen = 0;
         if (cur.scan < 0) {
             status = (int)cur.scan;
+        } else if constexpr (kG) {
+            const uint8_t* rec = cur.loc.in + cur.o0;
+            clen = (int)be32_global(rec);
+            const uintptr_t b0 = (uintptr_t)(rec + 4);
+            const GblRec src{b0, (b0 + (uintptr_t)clen - 1) & ~(uintptr_t)3};
+            if (!(VAR & 64))
+                lz4_exec_block(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
         } else {
             clen = (int)(((uint32_t)C[0] << 24) | ((uint32_t)C[1] << 16) | ((uint32_t)C[2] << 8) | C[3]);
             if (!(VAR & 64))
-                lz4_exec_block(Cbuf, cp + 4, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
+                lz4_exec_block(LdsRec{Cbuf}, cp + 4, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan,
+                               cur_pos, lane);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -698,12 +777,21 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         bool nxt2_in_regs = false;
         uint32_t nxt_pos = 0;
         if (next < nb) {
-            nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
-            if (nn < nb) {
-                nxt2 = span_from(a, O, nb);
-                if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
-                nxt2_in_regs = span_fits(a, nxt2);
-                if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
+            if constexpr (kG) {
+                nxt_pos = pref_pos;
+                if (nn < nb) {
+                    nxt2 = span_from(a, O, nb);
+                    if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                    pref_pos = nxt2.loc.seq[nxt2.o0 / 3 + lane];
+                }
+            } else {
+                nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
+                if (nn < nb) {
+                    nxt2 = span_from(a, O, nb);
+                    if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                    nxt2_in_regs = span_fits(a, nxt2);
+                    if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
+                }
             }
         }
         if (status == 0 && !(VAR & 8)) {
@@ -788,6 +876,7 @@ __global__ __launch_bounds__(256) void k_decode_finish(const int64_t* __restrict
         else
             *result = end + tail;
     }
+    finish_visible();
 }
 
 }  // namespace
@@ -890,14 +979,18 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     const Layout& L = a.L;
     // decoded block + record (header, payload, 16-byte alignment slack)
     const size_t rec = (((size_t)a.maxlen + 4 + 32 + 15) & ~(size_t)15);
-    const size_t lds = (size_t)a.cap + 16 + rec;
+    // phase 2 reads each record straight from global memory, so the LDS holds
+    // only the decoded block: 18 resident waves per CU instead of 9 (A/B
+    // variant 16: the record staged in LDS, as before)
+    const bool grec = tuning_variant() != 16;
+    size_t lds = (size_t)a.cap + 16 + (grec ? 0 : rec);
     const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
     const void* fn = nullptr;
 #define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
     switch (ek) {
-        case 1: fn = BSHUF_DEC(1, 0); break;
+        case 1: fn = grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0); break;
         case 2:
-            fn = BSHUF_DEC(2, 0);
+            fn = grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0);
 #ifdef BSHUF_DIAG
             // diagnostic build only -- ABLATIONS for timing, wrong output:
             // 8 no output stores, 64 no sequence execution
@@ -907,19 +1000,27 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
 #endif
             break;
         case 4:
-            fn = BSHUF_DEC(4, 0);
+            fn = grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0);
 #ifdef BSHUF_DIAG
             if (diag_variant() == 8) fn = BSHUF_DEC(4, 8);
             if (diag_variant() == 64) fn = BSHUF_DEC(4, 64);
             if (diag_variant() == 72) fn = BSHUF_DEC(4, 72);
 #endif
             break;
-        case 8: fn = BSHUF_DEC(8, 0); break;
-        default: fn = BSHUF_DEC(0, 0); break;
+        case 8: fn = grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0); break;
+        default: fn = grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0); break;
     }
 #undef BSHUF_DEC
     hipError_t e = scan_impl(a, nb, s);
     if (e != hipSuccess) return e;
+#ifdef BSHUF_DIAG
+    // occupancy experiment: BSHUF_DIAG_DEC_WAVES=w pads the LDS request so
+    // that at most w waves fit a CU
+    if (const char* w = getenv("BSHUF_DIAG_DEC_WAVES")) {
+        const size_t want = (size_t)(160 * 1024 / atoi(w)) & ~(size_t)1023;
+        if (want > lds) lds = want;
+    }
+#endif
     if (lds > 65536) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -948,6 +1049,7 @@ __global__ __launch_bounds__(64) void k_decode_finish_batch(const int64_t* __res
     if (ok)
         for (int64_t i = threadIdx.x; i < g.tail; i += blockDim.x) tail_dst[i] = g.in[end + i];
     if (threadIdx.x == 0) *g.result = last_bad >= 0 ? status[last_bad] : (!ok ? -91 : end + g.tail);
+    finish_visible();
 }
 
 }  // namespace

@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 
 #include "launch.h"
@@ -43,7 +44,10 @@ constexpr int kTableBytes = 16384;  // byU16: 8192 x u16, byU32: 4096 x u32
 // s_memtime cycle sums and event counters.  The product build compiles these
 // macros to nothing.
 #ifdef BSHUF_DIAG
-__device__ unsigned long long g_diag[32];
+// 64 copies of the 32 counters, picked by workgroup, so the flush atomics of
+// 1,536 resident waves do not serialise on 32 addresses.
+constexpr int kDiagCopies = 64;
+__device__ unsigned long long g_diag[kDiagCopies * 32];
 #define DIAG_DECL                                   \
     uint64_t _dt = __builtin_amdgcn_s_memtime();    \
     uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};    \
@@ -59,11 +63,33 @@ __device__ unsigned long long g_diag[32];
     do {                                                                    \
         if (lane == 0)                                                      \
             for (int _i = 0; _i < 8; _i++) {                                \
-                atomicAdd(&g_diag[_i], (unsigned long long)_acc[_i]);       \
-                atomicAdd(&g_diag[8 + _i], (unsigned long long)_cnt[_i]);   \
+                atomicAdd(&g_diag[(blockIdx.x % kDiagCopies) * 32 + _i],   \
+                          (unsigned long long)_acc[_i]);                    \
+                atomicAdd(&g_diag[(blockIdx.x % kDiagCopies) * 32 + 8 + _i], \
+                          (unsigned long long)_cnt[_i]);                    \
             }                                                               \
     } while (0)
+// kernel-level phases of k_lz4_encode (slots 16..19): zero + transpose,
+// parse, emission + copy-out, everything else
+#define KDIAG_DECL                                   \
+    uint64_t _kt = __builtin_amdgcn_s_memtime();     \
+    uint64_t _kacc[4] = {0, 0, 0, 0};
+#define KSTAMP(i)                                       \
+    do {                                                \
+        const uint64_t _n = __builtin_amdgcn_s_memtime(); \
+        _kacc[i] += _n - _kt;                           \
+        _kt = _n;                                       \
+    } while (0)
+#define KDIAG_FLUSH                                                                     \
+    do {                                                                                \
+        if (lane == 0)                                                                  \
+            for (int _i = 0; _i < 4; _i++)                                              \
+                atomicAdd(&g_diag[(blockIdx.x % kDiagCopies) * 32 + 16 + _i], _kacc[_i]); \
+    } while (0)
 #else
+#define KDIAG_DECL
+#define KSTAMP(i) ((void)0)
+#define KDIAG_FLUSH ((void)0)
 #define DIAG_DECL
 #define STAMP(i) ((void)0)
 #define COUNT(i, v) ((void)0)
@@ -420,7 +446,7 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
 // Returns the compressed size, or -1 when the emitter ran out of descriptor
 // slots.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1, notLimited
 // output.
-template <bool WIDE, bool READBACK, class Emit>
+template <bool WIDE, bool READBACK, int OPT, class Emit>
 __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T, Emit& em,
                                 const int lane) {
     DIAG_DECL
@@ -583,7 +609,15 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                 pre = lds_rd32(D, min(ip + 1 + lane, n));
                 const uint32_t va0 = lds_rd32(D, min(ip + 4 * lane, n));
                 uint32_t c2 = 0;
-                if (lane == 0) {
+                if constexpr ((OPT & 8) != 0) {
+                    // plain ops, in order: the read sees the ip-2 insert when
+                    // both hashes agree
+                    if (lane == 0) {
+                        T.put(h2, (uint32_t)(ip - 2));
+                        c2 = T.get(h0);
+                        T.put(h0, (uint32_t)ip);
+                    }
+                } else if (lane == 0) {
                     T.put(h2, (uint32_t)(ip - 2));
                     c2 = T.exchange(h0, (uint32_t)ip);
                 }
@@ -748,7 +782,9 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
             issue_block_loads<EK>(R, blk_src(blk), m0 / 8, lane);
     }
 
+    KDIAG_DECL
     for (;;) {
+        KSTAMP(3);
         const int m = blk_m(blk);
         const int n = m * E;
         const int P = m / 8;
@@ -800,6 +836,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
             }
         }
 
+        KSTAMP(0);
         uint8_t* out = a.scratch + blk * a.slot;
         const Table<WIDE> T{L0};
         int c = -1;
@@ -809,7 +846,8 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if constexpr (kDesc) {
             if (a.desc_ok && 4 + lz4_bound(n) + 15 <= kTableBytes) {
                 EmitDesc em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
+                c = lz4_encode_block<WIDE, kReadback, (VAR & 8)>(D, n, T, em, lane);
+                KSTAMP(1);
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -833,15 +871,17 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         }
         if (c < 0) {
             EmitBytes em{out + 4, D, lane};
-            c = lz4_encode_block<WIDE, kReadback>(D, n, T, em, lane);
+            c = lz4_encode_block<WIDE, kReadback, (VAR & 8)>(D, n, T, em, lane);
             if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         }
         if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        KSTAMP(2);
         if (next >= nb) break;
         blk = next;
     }
+    KDIAG_FLUSH;
 }
 
 // Move each [BE32 c][c bytes] record from its scratch slot to out + offs[k].
@@ -942,6 +982,7 @@ __global__ void k_encode_finish(const uint64_t* offs, int64_t nblocks, const uin
     const uint64_t end = offs[nblocks];
     for (int i = threadIdx.x; i < tail; i += blockDim.x) out[end + i] = tail_src[i];
     if (threadIdx.x == 0) *result = (int64_t)end + tail;
+    finish_visible();
 }
 
 // Batch: one workgroup per stream.
@@ -952,6 +993,7 @@ __global__ void k_encode_finish_batch(const uint64_t* offs, const Seg* segs, int
     const uint8_t* tail_src = g.in + (g.nfull * (int64_t)bs + g.last) * E;
     for (int i = threadIdx.x; i < g.tail; i += blockDim.x) g.out[end + i] = tail_src[i];
     if (threadIdx.x == 0) *g.result = (int64_t)end + g.tail;
+    finish_visible();
 }
 
 // Device check of the property Table::exchange relies on: same-address lanes
@@ -1045,6 +1087,7 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 2) return launch_enc_t<2, false, 2>(a, nb, lds, s);
         if (v == 4) return launch_enc_t<2, false, 4>(a, nb, lds, s);
         if (v == 128) return launch_enc_t<2, false, 128>(a, nb, lds, s);
+        if (v == 8) return launch_enc_t<2, false, 8>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
@@ -1056,6 +1099,18 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
+#ifdef BSHUF_DIAG
+    // occupancy experiment: BSHUF_DIAG_WAVES=w pads the LDS request so that at
+    // most w waves fit a CU
+    if (const char* w = getenv("BSHUF_DIAG_WAVES")) {
+        const size_t want = (size_t)(160 * 1024 / atoi(w)) & ~(size_t)1023;
+        if (want > lds) {
+            lds = want;
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        }
+    }
+#endif
     const int64_t grid = persistent_grid(reinterpret_cast<const void*>(fn), kWave, lds, nb);
     ProfScope prof("k_lz4_encode", s);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kWave), lds, s, a, nb);
@@ -1233,10 +1288,13 @@ hipError_t launch_seg_map(const Seg* segs, int nsegs, uint32_t* map, bool chunks
 #ifdef BSHUF_DIAG
 // Diagnostic build only: read (and reset) the encoder's phase counters.
 extern "C" int bshuf_diag_read(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bshuf::g_diag), sizeof(unsigned long long) * 32) !=
-        hipSuccess)
-        return -1;
-    unsigned long long z[32] = {0};
+    static unsigned long long all[bshuf::kDiagCopies * 32];
+    if (hipMemcpyFromSymbol(all, HIP_SYMBOL(bshuf::g_diag), sizeof all) != hipSuccess) return -1;
+    for (int i = 0; i < 32; i++) {
+        out[i] = 0;
+        for (int c = 0; c < bshuf::kDiagCopies; c++) out[i] += all[c * 32 + i];
+    }
+    static const unsigned long long z[bshuf::kDiagCopies * 32] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(bshuf::g_diag), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -61,12 +61,24 @@ static int g_diag_variant = 0;
 int diag_variant() { return g_diag_variant; }
 #endif
 
+constexpr int64_t kLdsGranule = 1280;
+constexpr int64_t kLdsPerCu = 160 * 1024;
+
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work) {
     int dev = 0, cus = 256, per = 1;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess || per < 1)
         per = 1;
+    // gfx950 allocates LDS in 1,280-byte granules (measured, tools/lds_resid.hip);
+    // the runtime's occupancy query assumes finer ones and can promise one
+    // workgroup more per CU than fits, which leaves a second, mostly idle
+    // round of persistent workgroups
+    if (lds > 0) {
+        const int64_t g = ((int64_t)lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule;
+        const int fit = (int)(kLdsPerCu / g);
+        if (fit >= 1 && per > fit) per = fit;
+    }
     const int64_t g = (int64_t)cus * per;
     return work < g ? (work > 0 ? work : 1) : g;
 }
@@ -95,9 +107,11 @@ using namespace bshuf;
 extern "C" {
 
 int bshuf_set_variant(int v) {
-    // 2 inline LZ4 emitter, 4 one-group-per-lane transpose, 128 insert/readback
+    // 2 inline LZ4 emitter, 4 one-group-per-lane transpose, 8 re-test table
+    // lookup by plain LDS ops, 16 decoder stages each record in LDS,
+    // 128 insert/readback
     // search window (the fallback for devices without lane-ordered LDS atomics)
-    if (v != 0 && v != 2 && v != 4 && v != 128) return -71;
+    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 128) return -71;
     t_variant = v;
     return 0;
 }

@@ -140,7 +140,25 @@ static int regress(const char* dir, const char* out) {
         unsigned char* back = malloc(no + 16);
         good2 = good2 && H5Dread(d, type, H5S_ALL, H5S_ALL, H5P_DEFAULT, back) >= 0 &&
                 memcmp(back, orig, no) == 0;
-        if (!good2) fprintf(stderr, "DECODE mismatch %s/%s\n", ver, name);
+        if (!good2) {
+            size_t first = no, diff = 0;
+            for (size_t i = 0; i < no; i++)
+                if (back[i] != orig[i]) {
+                    if (first == no) first = i;
+                    diff++;
+                }
+            fprintf(stderr, "DECODE mismatch %s/%s (%zu of %zu bytes differ, first at %zu)\n", ver,
+                    name, diff, no, first);
+            if (getenv("H5H_DUMP") && first < no) {
+                fprintf(stderr, " got   ");
+                for (size_t i = first; i < no && i < first + 32; i++) fprintf(stderr, "%02x", back[i]);
+                fprintf(stderr, "\n orig  ");
+                for (size_t i = first; i < no && i < first + 32; i++) fprintf(stderr, "%02x", orig[i]);
+                fprintf(stderr, "\n chunk ");
+                for (size_t i = first; i + 12 < nc && i < first + 32; i++) fprintf(stderr, "%02x", chunk[12 + i]);
+                fprintf(stderr, "\n");
+            }
+        }
         H5Dclose(d);
         H5Tclose(type);
         ok += good && good2;

@@ -38,6 +38,10 @@ print("blocks", blocks, "ratio", x.numel() * x.element_size() / c.numel())
 for i, nm in enumerate(names):
     print("%-12s %8.0f cyc/block  %5.1f%%" % (nm, v[i] / blocks, 100.0 * v[i] / max(tot, 1)))
 print("parse cycles/block %.0f" % (tot / blocks))
+kn = ["zero+transpose", "parse", "emit+copy-out", "loop/other"]
+ktot = sum(v[16:20])
+for i, nm in enumerate(kn):
+    print("kernel %-15s %8.0f cyc/block  %5.1f%%" % (nm, v[16 + i] / blocks, 100.0 * v[16 + i] / max(ktot, 1)))
 for i, nm in enumerate(cnt):
     print("%-18s %8.2f per block" % (nm, v[8 + i] / blocks))
 print("kernel ms", {k: round(t / c_, 3) for k, (c_, t) in prof.items()})
