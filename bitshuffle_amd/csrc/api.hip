@@ -7,6 +7,7 @@
 // entry point returns -70.  The *_dev entry points take device pointers and
 // only enqueue work.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -625,10 +626,11 @@ bool stage_init(HostCtx& c) {
 
 // Appends `n` bytes host -> device at dst (piece by piece; returns at once
 // after the last memcpy, the DMA may still run).
-// Before a device->host copy of results: every XCD's L2 written back to
-// memory (a system-scope release per workgroup; 256 workgroups reach all 8
-// XCDs).  Without it the copy was seen to read stale bytes of lines the
-// stream's last kernel had just written (finish_visible, bshuf_dev.h).
+// Every XCD's L2 written back to memory and invalidated (a system-scope
+// release + acquire per workgroup; 256 workgroups reach all 8 XCDs): after the
+// runtime's host->device copies into the reused per-thread buffers and before
+// the device->host copy of results, so that neither side of a copy can meet a
+// line an L2 kept from an earlier call.
 __global__ __launch_bounds__(64) void k_host_release() { __threadfence_system(); }
 
 hipError_t host_visible(hipStream_t s) {
@@ -699,7 +701,8 @@ static int64_t transpose_host(const void* in, void* out, size_t size, size_t ele
     void* di = ctx_buf(HostCtx::kIn, bytes, s);
     void* dout = ctx_buf(HostCtx::kOut, bytes, s);
     if (!di || !dout) return -1;
-    if (h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) return kErrHip;
+    if (h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess || host_visible(s) != hipSuccess)
+        return kErrHip;
     const int64_t n = transpose_dev(di, dout, size, elem_size, block_size, s, fwd);
     if (n < 0) return n;
     if (host_visible(s) != hipSuccess || d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess)
@@ -732,7 +735,9 @@ int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const s
     void* ws = ctx_buf(HostCtx::kWs, wsb, s);
     int64_t* dres = (int64_t*)ctx_buf(HostCtx::kRes, 8, s);
     if (!di || !dout || !ws || !dres) return -1;
-    if (bytes && h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) return kErrHip;
+    if ((bytes && h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) ||
+        host_visible(s) != hipSuccess)
+        return kErrHip;
     const int64_t e = bshuf_compress_lz4_dev(di, dout, size, elem_size, block_size, ws, wsb, dres,
                                              nullptr, s);
     if (e < 0) return e;
@@ -799,10 +804,15 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const
     if (in_nbytes > max_in) return -91;
     if ((in_nbytes > issued && h2d(di + issued, i8 + issued, in_nbytes - issued, s) != hipSuccess) ||
         (p.nb && hipMemcpyAsync(doffs, offs.data(), (size_t)p.nb * 8, hipMemcpyHostToDevice, s) !=
-                     hipSuccess))
+                     hipSuccess) ||
+        host_visible(s) != hipSuccess)
         return kErrHip;
+    // the thread's cached workspace (no stream-ordered allocation per call)
+    const size_t wsb = bshuf_decompress_lz4_dev_workspace(in_nbytes, size, elem_size, block_size);
+    void* ws = ctx_buf(HostCtx::kWs, wsb, s);
+    if (!ws) return -1;
     const int64_t e = bshuf_decompress_lz4_dev(di, in_nbytes, dout, size, elem_size, block_size,
-                                               nullptr, 0, dres, doffs, s);
+                                               ws, wsb, dres, doffs, s);
     if (e < 0) return e;
     int64_t res = 0;
     if (host_visible(s) != hipSuccess ||

@@ -32,6 +32,8 @@ int diag_variant();  // timing ablations (wrong output), diag build only
 // Workgroups for a persistent launch: resident blocks per CU (occupancy API,
 // dynamic LDS included) x CUs of the current device, capped by the work.
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work);
+// hipMemsetAsync's job done by a kernel (prof.hip)
+hipError_t dev_fill(void* p, int v, size_t n, hipStream_t s);
 
 // One independent framed stream of a batch (bshuf_*_lz4_batch_dev).  All
 // streams of a batch share elem_size and block_size; global block k of the

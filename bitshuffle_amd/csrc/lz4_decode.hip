@@ -688,6 +688,25 @@ __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     a.status[k] = st;
 }
 
+// VAR & 32: one dword of every 64-byte line of a record, loaded two blocks
+// ahead so that phase 2's reads of it hit L2; the values are never used.
+struct Touch {
+    uint32_t v0, v1;
+};
+__device__ __forceinline__ Touch touch_record(const Span& sp, int lane) {
+    Touch t{0u, 0u};
+    const int64_t len = sp.o1 - sp.o0;
+    const uintptr_t b = (uintptr_t)(sp.loc.in + sp.o0) & ~(uintptr_t)63;
+    const uintptr_t e = (uintptr_t)(sp.loc.in + sp.o1);
+    const uintptr_t a0 = b + 64 * (uintptr_t)lane, a1 = a0 + 64 * kWave;
+    if (len > 0 && a0 < e) t.v0 = *(gbl32c*)a0;
+    if (len > 0 && a1 < e) t.v1 = *(gbl32c*)a1;
+    return t;
+}
+__device__ __forceinline__ void touch_done(const Touch& t) {
+    asm volatile("" : : "v"(t.v0), "v"(t.v1));
+}
+
 // Returns this lane's token position of the record (two-phase path).
 __device__ __forceinline__ uint32_t land_record(const PayRegs& R, bool in_regs, const DecArgs& a,
                                                 const Span& sp, lds8* Cbuf, int lane) {
@@ -734,10 +753,13 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     Span nxt = {};
     bool nxt_in_regs = false;
     uint32_t pref_pos = 0;  // kG: token position of block `next`, loaded a parse early
+    constexpr bool kTouch = (VAR & 32) != 0;
+    Touch t_cur{0u, 0u}, t_nxt{0u, 0u}, t_nxt2{0u, 0u};
     if (next < nb) {
         nxt = span_from(a, issue_offs(a, next, nb, lane), nb);
         if constexpr (kG) {
             pref_pos = nxt.loc.seq[nxt.o0 / 3 + lane];
+            if constexpr (kTouch) t_nxt = touch_record(nxt, lane);
         } else {
             nxt_in_regs = span_fits(a, nxt);
             if (nxt_in_regs) issue_pay(R, a, nxt, lane);
@@ -757,6 +779,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         if (cur.scan < 0) {
             status = (int)cur.scan;
         } else if constexpr (kG) {
+            if constexpr (kTouch) touch_done(t_cur);  // this block's (issued two blocks ago)
             const uint8_t* rec = cur.loc.in + cur.o0;
             clen = (int)be32_global(rec);
             const uintptr_t b0 = (uintptr_t)(rec + 4);
@@ -783,6 +806,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                     nxt2 = span_from(a, O, nb);
                     if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
                     pref_pos = nxt2.loc.seq[nxt2.o0 / 3 + lane];
+                    if constexpr (kTouch) t_nxt2 = touch_record(nxt2, lane);
                 }
             } else {
                 nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
@@ -850,6 +874,10 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
         next = nn;
         nxt = nxt2;
         nxt_in_regs = nxt2_in_regs;
+        if constexpr (kTouch) {
+            t_cur = t_nxt;
+            t_nxt = t_nxt2;
+        }
     }
 }
 
@@ -908,11 +936,11 @@ int64_t idx_win_lds(uint32_t maxlen) {
 // Index rebuild over nch chunks (of one stream, or of every stream of a batch).
 hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, const DecodeBufs& b,
                       hipStream_t s) {
-    hipError_t e = hipMemsetAsync(b.idx_err, 0, sizeof(int64_t) * (size_t)nsegs, s);
+    hipError_t e = dev_fill(b.idx_err, 0, sizeof(int64_t) * (size_t)nsegs, s);
     if (e != hipSuccess || nb == 0) return e;
     // offsets a broken chain never reaches stay at the all-ones sentinel
     // (clamp_span turns them into -1001 without reading the stream)
-    e = hipMemsetAsync(b.offs, 0xFF, (size_t)nb * sizeof(uint64_t), s);
+    e = dev_fill(b.offs, 0xFF, (size_t)nb * sizeof(uint64_t), s);
     if (e != hipSuccess || nch == 0) return e;
     {
         ProfScope prof("k_idx_exits", s);
@@ -930,7 +958,7 @@ hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, cons
         hipLaunchKernelGGL(k_idx_walk, dim3(wg), dim3(64), 0, s, x, nch, b.exits, b.cnt,
                            (const uint64_t*)nullptr, (uint64_t*)nullptr, 0);
     }
-    e = hipMemsetAsync(b.cnt + nch, 0, sizeof(uint64_t), s);
+    e = dev_fill(b.cnt + nch, 0, sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     size_t tmp = b.scan_tmp_bytes;
     {
@@ -983,32 +1011,34 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     // only the decoded block: 18 resident waves per CU instead of 9 (A/B
     // variant 16: the record staged in LDS, as before)
     const bool grec = tuning_variant() != 16;
+    // ... and touches each record's lines two blocks ahead (variant 32: not)
+    const bool touch = grec && tuning_variant() != 32;
     size_t lds = (size_t)a.cap + 16 + (grec ? 0 : rec);
     const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
     const void* fn = nullptr;
 #define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
     switch (ek) {
-        case 1: fn = grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0); break;
+        case 1: fn = touch ? BSHUF_DEC(1, 48) : (grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0)); break;
         case 2:
-            fn = grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0);
+            fn = touch ? BSHUF_DEC(2, 48) : (grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0));
 #ifdef BSHUF_DIAG
             // diagnostic build only -- ABLATIONS for timing, wrong output:
             // 8 no output stores, 64 no sequence execution
-            if (diag_variant() == 8) fn = BSHUF_DEC(2, 8);
-            if (diag_variant() == 64) fn = BSHUF_DEC(2, 64);
-            if (diag_variant() == 72) fn = BSHUF_DEC(2, 72);
+            if (diag_variant() == 8) fn = BSHUF_DEC(2, 56);
+            if (diag_variant() == 64) fn = BSHUF_DEC(2, 112);
+            if (diag_variant() == 72) fn = BSHUF_DEC(2, 120);
 #endif
             break;
         case 4:
-            fn = grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0);
+            fn = touch ? BSHUF_DEC(4, 48) : (grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0));
 #ifdef BSHUF_DIAG
-            if (diag_variant() == 8) fn = BSHUF_DEC(4, 8);
-            if (diag_variant() == 64) fn = BSHUF_DEC(4, 64);
-            if (diag_variant() == 72) fn = BSHUF_DEC(4, 72);
+            if (diag_variant() == 8) fn = BSHUF_DEC(4, 56);
+            if (diag_variant() == 64) fn = BSHUF_DEC(4, 112);
+            if (diag_variant() == 72) fn = BSHUF_DEC(4, 120);
 #endif
             break;
-        case 8: fn = grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0); break;
-        default: fn = grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0); break;
+        case 8: fn = touch ? BSHUF_DEC(8, 48) : (grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0)); break;
+        default: fn = touch ? BSHUF_DEC(0, 48) : (grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0)); break;
     }
 #undef BSHUF_DEC
     hipError_t e = scan_impl(a, nb, s);
@@ -1058,7 +1088,7 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
                          hipStream_t s) {
     const int64_t nb = L.nblocks();
-    hipError_t e = hipMemsetAsync(b.bad, 0xFF, sizeof(long long), s);  // -1
+    hipError_t e = dev_fill(b.bad, 0xFF, sizeof(long long), s);  // -1
     if (e != hipSuccess) return e;
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
@@ -1084,7 +1114,7 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
 hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
                                const Layout& L, const DecodeBufs& b, hipStream_t s) {
     const int64_t nb = L.nfull;
-    hipError_t e = hipMemsetAsync(b.bad, 0xFF, sizeof(long long) * (size_t)nsegs, s);
+    hipError_t e = dev_fill(b.bad, 0xFF, sizeof(long long) * (size_t)nsegs, s);
     if (e != hipSuccess) return e;
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;

@@ -1189,7 +1189,7 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
         }
         if (e != hipSuccess) return e;
     }
-    e = hipMemsetAsync(b.foot + nb, 0, sizeof(uint64_t), s);
+    e = dev_fill(b.foot + nb, 0, sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     size_t tmp = b.scan_tmp_bytes;
     {
@@ -1246,7 +1246,7 @@ hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
 #undef BSHUF_E
         if (e != hipSuccess) return e;
     }
-    e = hipMemsetAsync(b.foot + nb, 0, sizeof(uint64_t), s);
+    e = dev_fill(b.foot + nb, 0, sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
     size_t tmp = b.scan_tmp_bytes;
     {

@@ -249,7 +249,7 @@ hipError_t launch_encode_large(const uint8_t* in, const Layout& L, const EncodeB
     if (nb == 0) return hipSuccess;
     hipError_t e = launch_transpose(in, shuf, L, true, s);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(tables, 0, (size_t)nb * kLargeTableWords * 4, s);
+    e = dev_fill(tables, 0, (size_t)nb * kLargeTableWords * 4, s);
     if (e != hipSuccess) return e;
     ProfScope prof("k_lz4_encode_seq", s);
     hipLaunchKernelGGL(k_lz4_encode_seq, dim3((unsigned)nb), dim3(64), 0, s, shuf, L, b.scratch, b.slot,

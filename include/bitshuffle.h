@@ -103,7 +103,8 @@ void bshuf_prof_enable(int on);
 /* Selects, for the CALLING THREAD only, an alternative kernel variant for A/B
  * measurements: 0 default, 2 inline LZ4 emitter, 4 one-group-per-lane
  * transpose, 8 re-test table lookup by plain LDS ops, 16 decoder with each
- * record staged in LDS, 128 insert/read-back search window.  Every accepted variant
+ * record staged in LDS, 32 decoder without the record-line touch two blocks
+ * ahead, 128 insert/read-back search window.  Every accepted variant
  * produces identical bytes; anything else is rejected with -71. */
 int bshuf_set_variant(int v);
 size_t bshuf_prof_collect(char* buf, size_t len);
