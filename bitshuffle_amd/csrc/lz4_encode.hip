@@ -198,7 +198,8 @@ constexpr int kDescMax = 256;              // descriptor slots per block
 constexpr int kDescBytes = 8 * kDescMax;   // LDS behind the block
 
 // Sequence s's descriptor: two dwords in LDS (ip | off << 16, lit | mc << 16),
-// stored by lane 0.  The record size is not tracked during the parse:
+// stored by every lane (same address, same value: no exec-mask switch on the
+// parse's chain).  The record size is not tracked during the parse:
 // emit_sequences' prefix sum gives it.
 struct EmitDesc {
     lds32* desc;
@@ -207,10 +208,8 @@ struct EmitDesc {
     int la = 0;   // anchor of the last literal run
     __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
         if (ns >= kDescMax) return false;
-        if (lane == 0) {
-            ((lds64v*)desc)[ns] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
-                                        (uint32_t)(ip - anchor) | ((uint32_t)mc << 16)};
-        }
+        ((lds64v*)desc)[ns] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
+                                    (uint32_t)(ip - anchor) | ((uint32_t)mc << 16)};
         ns++;
         (void)op;
         return true;
@@ -609,19 +608,22 @@ __device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T,
                 pre = lds_rd32(D, min(ip + 1 + lane, n));
                 const uint32_t va0 = lds_rd32(D, min(ip + 4 * lane, n));
                 uint32_t c2 = 0;
-                if constexpr ((OPT & 8) != 0) {
-                    // plain ops, in order: the read sees the ip-2 insert when
-                    // both hashes agree
+                if constexpr ((OPT & 8) == 0) {
+                    // plain ops by every lane (same address, same value; the
+                    // read is a broadcast), in order: the read sees the ip-2
+                    // insert when both hashes agree.  No exec-mask switch, and
+                    // c2 stays in a VGPR (no readfirstlane on the chain).
+                    T.put(h2, (uint32_t)(ip - 2));
+                    c2 = T.get(h0);
+                    T.put(h0, (uint32_t)ip);
+                } else {
+                    // A/B variant 8: lane 0 alone, one returning exchange
                     if (lane == 0) {
                         T.put(h2, (uint32_t)(ip - 2));
-                        c2 = T.get(h0);
-                        T.put(h0, (uint32_t)ip);
+                        c2 = T.exchange(h0, (uint32_t)ip);
                     }
-                } else if (lane == 0) {
-                    T.put(h2, (uint32_t)(ip - 2));
-                    c2 = T.exchange(h0, (uint32_t)ip);
+                    c2 = uni(c2);
                 }
-                c2 = uni(c2);
                 const bool near = !WIDE || c2 + kMaxDistance >= (uint32_t)ip;
                 if (near) {
                     co = test_and_count(D, n, ip, (int)c2, mlimit, lane, va0);

@@ -134,7 +134,7 @@ extern "C" {
 
 int bshuf_set_variant(int v) {
     // 2 inline LZ4 emitter, 4 one-group-per-lane transpose, 8 re-test table
-    // lookup by plain LDS ops, 16 decoder stages each record in LDS, 32
+    // lookup by lane 0's returning exchange, 16 decoder stages each record in LDS, 32
     // decoder without the two-blocks-ahead touch of each record's lines,
     // 128 insert/readback
     // search window (the fallback for devices without lane-ordered LDS atomics)

@@ -142,7 +142,8 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     read-back search window (the fallback when the LDS-atomic lane-order
     self-check fails), 2 the inline emitter (also the overflow path of the
     descriptor emitter), 4 the one-group-per-lane transpose, 8 the re-test
-    table lookup by plain LDS ops, 16 the decoder with each record staged in
+    table lookup by lane 0's returning exchange (the default: plain LDS ops by
+    every lane), 16 the decoder with each record staged in
     LDS (the default reads records from global memory), 32 the decoder
     without the two-blocks-ahead touch of each record's lines."""
     rng = np.random.default_rng(128)
