@@ -661,6 +661,46 @@ struct GReader {
     __device__ __forceinline__ uint32_t operator()(int p) { return gw_byte(g, P, clen, p); }
 };
 
+// Token positions of one lane's block, four per 16-byte store: entry i sits
+// in dword slot (ph + i) & 3 of its absolute 16-byte chunk, and a chunk is
+// stored whole once its slot 3 is filled -- unless it begins before the
+// block's first entry (that part belongs to the previous block's range), in
+// which case its entries go dword by dword, as do the last chunk's at flush.
+// A quarter of the scattered position stores (each costs a whole write
+// transaction, and on gfx9's in-order vmcnt every store issued before a
+// window load is waited for with it).
+struct SeqOut {
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    uint32_t* base;
+    int ph;  // dword phase of base within its 16-byte chunk
+    u32x4 buf;
+    __device__ __forceinline__ static uint32_t sel(const u32x4 b, int s) {
+        return s == 0 ? b.x : (s == 1 ? b.y : (s == 2 ? b.z : b.w));
+    }
+    __device__ __forceinline__ void put(int i, uint32_t v) {
+        const int s = (ph + i) & 3;
+        buf.x = s == 0 ? v : buf.x;
+        buf.y = s == 1 ? v : buf.y;
+        buf.z = s == 2 ? v : buf.z;
+        buf.w = s == 3 ? v : buf.w;
+        if (s == 3) {
+            if (i >= 3) {
+                *(gbl128*)(base + i - 3) = buf;
+            } else {
+                for (int j = ph; j < 4; j++) ((g32*)base)[j - ph] = sel(buf, j);
+            }
+        }
+    }
+    // entries [0, cnt) put; store those of the unfinished last chunk
+    __device__ __forceinline__ void flush(int cnt) {
+        const int s_end = (ph + cnt) & 3;  // slots [lo, s_end) of the last chunk pending
+        if (cnt <= 0 || s_end == 0) return;
+        const int lo = cnt < s_end ? ph : 0;
+        const int i0 = cnt - (s_end - lo);
+        for (int j = lo; j < s_end; j++) ((g32*)base)[i0 + j - lo] = sel(buf, j);
+    }
+};
+
 // status[k] = number of sequences, or the block's final error code (r - 1000
 // for an LZ4 failure, -91 when the block does not decode to exactly n bytes).
 // seq[offs[k]/3 + i] = payload position of sequence i's token (a sequence
@@ -682,7 +722,12 @@ __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
         rd.g.w0 = -(1 << 30);
         rd.P = loc.in + o0 + 4;
         rd.clen = (int)clen;
-        const int r = scan_block(rd, (int)clen, n, loc.seq + o0 / 3, cnt);
+        SeqOut out;
+        out.base = loc.seq + o0 / 3;
+        out.ph = (int)(((uintptr_t)out.base >> 2) & 3);
+        out.buf = u32x4{0u, 0u, 0u, 0u};
+        const int r = scan_block(rd, (int)clen, n, out, cnt);
+        out.flush(cnt);  // a rejected block's positions are never read
         st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
     }
     a.status[k] = st;

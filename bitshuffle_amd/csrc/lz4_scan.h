@@ -36,9 +36,10 @@ BSHUF_HD inline bool scan_len(Rd& rd, int& ip, int ilimit, bool initial_check, i
 // without the copies: the fast loop (2083-2209) and the safe loop (2215-2435)
 // check different margins, so both are followed to reach the same accept /
 // reject decision and error position.  Records each sequence's token position.
-// Returns op (bytes the block decodes to) or -(ip)-1.
-template <class Rd>
-BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, uint32_t* out, int& cnt) {
+// Returns op (bytes the block decodes to) or -(ip)-1.  Token positions go to
+// out.put(i, pos) in increasing i (a rejected block may have put one more).
+template <class Rd, class Out>
+BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, Out& out, int& cnt) {
     enum { kNone, kLit, kCopyMatch, kMatch };
     int ip = 0, op = 0;
     cnt = 0;
@@ -57,7 +58,7 @@ BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, uint32_t* ou
                 entry = kLit;
             }
             if (entry == kNone) {
-                out[cnt++] = (uint32_t)tp;
+                out.put(cnt++, (uint32_t)tp);
                 ip += len;
                 op += len;
                 off = (int)(rd(ip) | (rd(ip + 1) << 8));
@@ -85,7 +86,7 @@ BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, uint32_t* ou
             fast = false;  // the rest of the block runs in the safe loop
         } else {
             if (len != 15 && ip < clen - 16 && op <= n - 32) {
-                out[cnt++] = (uint32_t)tp;
+                out.put(cnt++, (uint32_t)tp);
                 ip += len;
                 op += len;
                 ml = tok & 15;
@@ -105,7 +106,7 @@ BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, uint32_t* ou
             }
         }
         if (entry == kLit) {
-            out[cnt++] = (uint32_t)tp;
+            out.put(cnt++, (uint32_t)tp);
             const int cpy = op + len;
             if (cpy > n - 12 || ip + len > clen - 8) {
                 // must be the last sequence: consume the input exactly
