@@ -463,7 +463,7 @@ static int64_t decomp_block(const uint8_t* in, uint8_t* out, size_t m, size_t E,
     if (nb < 0) return -1 - 1000; /* a negative size walks backwards: not followed */
     *c = (size_t)nb + 4;
     *p = m * E;
-    uint8_t* tmp = (uint8_t*)malloc(m * E ? m * E : 1);
+    uint8_t* tmp = (uint8_t*)malloc((m * E) != 0 ? (size_t)(m * E) : 1);
     if (!tmp) return -1;
     const int r = orc_lz4_decompress_block(in + 4, nb, tmp, (int)(m * E));
     if (r < 0) {
