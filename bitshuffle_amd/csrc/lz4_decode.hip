@@ -956,7 +956,7 @@ __global__ __launch_bounds__(256) void k_decode_finish(const int64_t* __restrict
 
 int64_t index_chunk_bytes(const Layout& L) {
     const int64_t foot = 4 + lz4_bound(L.bs * L.E);
-    int64_t ch = 64 * 1024;
+    int64_t ch = 128 * 1024;
     while (ch < 2 * foot) ch *= 2;
     return ch;
 }
