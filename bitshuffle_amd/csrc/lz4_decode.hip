@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     a.status[k] = st;
 }
 
-// VAR & 32: one dword of every 64-byte line of a record, loaded two blocks
+// VAR & 32: one dword of every 128-byte line of a record, loaded two blocks
 // ahead so that phase 2's reads of it hit L2; the values are never used.
 struct Touch {
     uint32_t v0, v1;
@@ -741,9 +741,9 @@ struct Touch {
 __device__ __forceinline__ Touch touch_record(const Span& sp, int lane) {
     Touch t{0u, 0u};
     const int64_t len = sp.o1 - sp.o0;
-    const uintptr_t b = (uintptr_t)(sp.loc.in + sp.o0) & ~(uintptr_t)63;
+    const uintptr_t b = (uintptr_t)(sp.loc.in + sp.o0) & ~(uintptr_t)127;
     const uintptr_t e = (uintptr_t)(sp.loc.in + sp.o1);
-    const uintptr_t a0 = b + 64 * (uintptr_t)lane, a1 = a0 + 64 * kWave;
+    const uintptr_t a0 = b + 128 * (uintptr_t)lane, a1 = a0 + 128 * kWave;
     if (len > 0 && a0 < e) t.v0 = *(gbl32c*)a0;
     if (len > 0 && a1 < e) t.v1 = *(gbl32c*)a1;
     return t;
