@@ -43,6 +43,8 @@ PROTOTYPES = {
     "bshuf_prof_enable": (None, [_int]),
     "bshuf_set_variant": (_int, [_int]),
     "bshuf_prof_collect": (_sz, [ctypes.c_char_p, _sz]),
+    "bshuf_host_poison": (_i64, [_int]),
+    "bshuf_host_xfer_stats": (None, [_vp]),
 }
 
 

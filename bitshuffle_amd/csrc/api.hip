@@ -1,51 +1,24 @@
-// api.hip -- the drop-in C-ABI (include/bitshuffle.h, include/bitshuffle_core.h).
-//
-// Host-pointer entry points keep the reference's contract exactly
-// (src/bitshuffle_core.c:2038-2062, src/bitshuffle.c:214-247): they stage the
-// buffers through device memory on a per-thread HIP stream and run the gfx950
-// kernels.  There is no CPU compute path: without a usable HIP device every
-// entry point returns -70.  The *_dev entry points take device pointers and
-// only enqueue work.
+// api.hip -- the device-resident C-ABI (include/bitshuffle.h,
+// include/bitshuffle_core.h): default block size, compress bound, the *_dev
+// and *_batch_dev entry points (device pointers, enqueue only).  The
+// host-pointer drop-in entry points live in host.hip.  There is no CPU compute
+// path: without a usable HIP device every entry point returns -70.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "../../include/bitshuffle.h"
 #include "launch.h"
+#include "plan.h"
 
 using namespace bshuf;
 
 namespace {
-
-constexpr int64_t kErrHip = -70;
-constexpr int64_t kErrUnsupported = -71;
-
-struct Plan {
-    Layout L;
-    int64_t tail;  // raw tail bytes
-    int64_t nb;    // nblocks
-};
-
-// Blocking of src/bitshuffle_core.c:1877-1931.
-int64_t make_plan(size_t size, size_t elem_size, size_t block_size, Plan& p) {
-    if (elem_size == 0) return kErrUnsupported;
-    if (block_size == 0) block_size = bshuf_default_block_size(elem_size);
-    if (block_size % kBlockedMult) return -81;
-    if (block_size * elem_size > (size_t)INT32_MAX / 2 || elem_size > 65536) return kErrUnsupported;
-    p.L.bs = (int32_t)block_size;
-    p.L.E = (int32_t)elem_size;
-    p.L.nfull = (int64_t)(size / block_size);
-    size_t last = size % block_size;
-    last -= last % kBlockedMult;
-    p.L.last = (int32_t)last;
-    p.tail = (int64_t)((size % kBlockedMult) * elem_size);
-    p.nb = p.L.nblocks();
-    return 0;
-}
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -59,21 +32,6 @@ struct Carver {
         return p;
     }
 };
-
-bool have_device() {
-    static int n = -1;
-    if (n < 0) {
-        int c = 0;
-        n = (hipGetDeviceCount(&c) == hipSuccess) ? c : 0;
-    }
-    return n > 0;
-}
-
-hipStream_t thread_stream() {
-    thread_local hipStream_t s = nullptr;
-    if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
-    return s;
-}
 
 // ---- workspace layouts -------------------------------------------------------
 size_t enc_ws(const Plan& p, EncodeBufs* b, uint8_t* base) {
@@ -118,12 +76,52 @@ size_t dec_ws(const Plan& p, int64_t blocks_end, int64_t in_nbytes, bool need_in
     return c.off;
 }
 
+// Workspace of a *_dev call made with ws == NULL: stream-ordered allocation,
+// freed stream-ordered when the call returns -- from the library's OWN memory
+// pool, whose release threshold keeps freed memory mapped for reuse.  The
+// device's default pool (release threshold 0) hands freed blocks back to the
+// OS at synchronisation points and maps memory again at the next allocation;
+// kernels working in such re-mapped workspaces produced wrong results early in
+// a process (round-2 host-path defect, DESIGN.md §4.2: 16 of 40 fresh HDF5
+// regression processes with the default pool, 0 of 40 with a pool that never
+// trims).  BSHUF_DIAG_POOL=default brings the default pool back for that
+// experiment only (tools/h5_repro.sh).
+hipMemPool_t workspace_pool() {
+    static hipMemPool_t pool = nullptr;
+    static bool tried = false;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> g(mu);
+    if (tried) return pool;
+    tried = true;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const char* e = getenv("BSHUF_DIAG_POOL");
+    if (e && !strcmp(e, "default")) {
+        (void)hipDeviceGetDefaultMemPool(&pool, dev);
+        return pool;
+    }
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+        pool = nullptr;
+        return nullptr;
+    }
+    uint64_t keep = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    return pool;
+}
+
 struct DevBuf {
     void* p = nullptr;
     hipStream_t s = nullptr;
     hipError_t alloc(size_t n, hipStream_t st) {
         s = st;
-        return hipMallocAsync(&p, n ? n : 1, st);
+        hipMemPool_t pool = workspace_pool();
+        if (!pool) return hipErrorOutOfMemory;
+        return hipMallocFromPoolAsync(&p, n ? n : 1, pool, st);
     }
     ~DevBuf() {
         if (p) (void)hipFreeAsync(p, s);
@@ -371,36 +369,6 @@ size_t dec_batch_ws(const BatchPlan& bp, DecodeBufs* b, Seg** dsegs, uint32_t** 
     return c.off;
 }
 
-// Uploads a batch's segment table without blocking the host: the bytes go
-// through a per-thread pinned staging buffer, which is reused only after the
-// event of its previous copy has completed.
-hipError_t upload_table(const void* host, size_t bytes, void* dev, hipStream_t s) {
-    struct Stage {
-        void* p = nullptr;
-        size_t cap = 0;
-        hipEvent_t ev = nullptr;
-        bool pending = false;
-    };
-    thread_local Stage st;
-    if (st.pending && hipEventSynchronize(st.ev) != hipSuccess) return hipErrorUnknown;
-    st.pending = false;
-    if (st.cap < bytes) {
-        if (st.p) (void)hipHostFree(st.p);
-        st.p = nullptr;
-        st.cap = 0;
-        if (hipHostMalloc(&st.p, bytes, hipHostMallocCoherent) != hipSuccess) return hipErrorOutOfMemory;
-        st.cap = bytes;
-    }
-    if (!st.ev && hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) != hipSuccess)
-        return hipErrorUnknown;
-    memcpy(st.p, host, bytes);
-    hipError_t e = hipMemcpyAsync(dev, st.p, bytes, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return e;
-    e = hipEventRecord(st.ev, s);
-    st.pending = e == hipSuccess;
-    return e;
-}
-
 // Caller workspace, or a stream-ordered allocation owned by `own`.
 int64_t get_ws(void*& ws, size_t ws_bytes, size_t need, DevBuf& own, hipStream_t s) {
     if (!ws) {
@@ -454,7 +422,7 @@ int64_t bshuf_compress_lz4_batch_dev(const void* const* in, void* const* out, co
     Seg* dsegs = nullptr;
     uint32_t* blk_seg = nullptr;
     enc_batch_ws(bp, &b, &dsegs, &blk_seg, (uint8_t*)ws);
-    if (upload_table(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
+    if (stage_upload(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
         launch_seg_map(dsegs, (int)count, blk_seg, false, s) != hipSuccess ||
         launch_encode_batch(dsegs, bp.segs.data(), (int)count, blk_seg, bp.L, b, block_offsets, s) !=
             hipSuccess)
@@ -497,7 +465,7 @@ int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_n
     Seg* dsegs = nullptr;
     uint32_t *blk_seg = nullptr, *chunk_seg = nullptr;
     dec_batch_ws(bp, &b, &dsegs, &blk_seg, &chunk_seg, (uint8_t*)ws);
-    if (upload_table(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
+    if (stage_upload(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
         launch_seg_map(dsegs, (int)count, blk_seg, false, s) != hipSuccess ||
         launch_seg_map(dsegs, (int)count, chunk_seg, true, s) != hipSuccess ||
         launch_index_batch(dsegs, (int)count, chunk_seg, bp.L, bp.nchunks, b, s) != hipSuccess ||
@@ -513,315 +481,6 @@ int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first, 
     return launch_synth(out, n_elem, gen, first, seed, (hipStream_t)stream) == hipSuccess
                ? 0
                : kErrHip;
-}
-
-// ---------------------------------------------------------------------------
-// host-pointer drop-in entry points
-// ---------------------------------------------------------------------------
-
-}  // extern "C"
-
-namespace {
-
-// Per-thread state of the host-pointer entry points: one HIP stream and
-// grow-only device buffers, so a caller that hands over chunk after chunk (the
-// HDF5 filter: one call per chunk) allocates nothing after the first call.
-// The buffers live until process exit (freeing device memory from a
-// thread-exit destructor could race the HIP runtime's own teardown).
-struct HostCtx {
-    enum { kIn, kOut, kWs, kOffs, kRes, kN };
-    void* buf[kN] = {};
-    size_t cap[kN] = {};
-    std::vector<uint64_t> offs;
-    // pinned double-buffered staging (host memcpy of piece i+1 overlaps the
-    // DMA of piece i); created on first use
-    void* pin[2] = {};
-    hipEvent_t ev[2] = {};
-    bool pending[2] = {};
-    // completion of each device->host piece: a fresh event per piece from a
-    // ring, never one event re-recorded while its previous recording may
-    // still be waited on (observed to complete early on the ROCm 7.2 runtime)
-    hipEvent_t dev_ring[8] = {};
-    unsigned ring_pos = 0;
-};
-
-HostCtx& host_ctx() {
-    thread_local HostCtx* c = new HostCtx();
-    return *c;
-}
-
-void* ctx_buf(int i, size_t n, hipStream_t s) {
-    HostCtx& c = host_ctx();
-    if (n == 0) n = 1;
-    if (c.buf[i] && c.cap[i] >= n) return c.buf[i];
-    if (c.buf[i]) {
-        (void)hipStreamSynchronize(s);
-        (void)hipFree(c.buf[i]);
-        c.buf[i] = nullptr;
-        c.cap[i] = 0;
-    }
-    const size_t want = std::max(n, c.cap[i] + c.cap[i] / 4);
-    if (hipMalloc(&c.buf[i], want) != hipSuccess) {
-        c.buf[i] = nullptr;
-        return nullptr;
-    }
-    c.cap[i] = want;
-    return c.buf[i];
-}
-
-// Host <-> device copies go in pieces through two pinned staging buffers of
-// the thread: the host memcpy of one piece overlaps the DMA of the other.
-// Copying from a caller's pageable buffer directly makes the runtime pin its
-// pages on every call -- for the fresh per-chunk buffers HDF5 hands a filter
-// that costs more than the copy itself.  BSHUF_HOST_STAGING=0 copies directly.
-constexpr size_t kStagePiece = 4u << 20;
-
-// bit 1: host->device staged (default), bit 2: device->host staged.  The
-// staged device->host copy is OFF by default: on the ROCm 7.2 runtime a
-// decoded chunk read back through it came out with a ~0.5 MB stale stretch
-// in about one call in ten (tools/stage_check3.py, not understood yet); the
-// direct copy into the caller's pageable buffer never did.
-int staging_mode() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("BSHUF_HOST_STAGING");
-        on = !e ? 1 : (e[0] == '0' ? 0 : (!strcmp(e, "h2d") ? 1 : (!strcmp(e, "d2h") ? 2 : 3)));
-    }
-    return on;
-}
-
-// Waits for a staging copy: its event, or (BSHUF_STAGE_SYNC=stream) the
-// whole stream.
-hipError_t wait_ev(hipEvent_t e, hipStream_t s) {
-    static int mode = -1;
-    if (mode < 0) {
-        const char* v = getenv("BSHUF_STAGE_SYNC");
-        mode = v && !strcmp(v, "stream") ? 1 : 0;
-    }
-    return mode ? hipStreamSynchronize(s) : hipEventSynchronize(e);
-}
-
-// The staging buffers are COHERENT (fine-grained) pinned memory: the default
-// (coarse-grained) kind lets the GPU's device->host writes bypass the CPU
-// caches, so a buffer the CPU has just read can be re-read stale after the
-// next DMA into it -- observed as silently wrong decompressed pieces.
-bool stage_init(HostCtx& c) {
-    for (int b = 0; b < 2; b++) {
-        if (!c.pin[b] && hipHostMalloc(&c.pin[b], kStagePiece, hipHostMallocCoherent) != hipSuccess) {
-            c.pin[b] = nullptr;
-            return false;
-        }
-        if (!c.ev[b] && hipEventCreateWithFlags(&c.ev[b], hipEventDisableTiming) != hipSuccess) {
-            c.ev[b] = nullptr;
-            return false;
-        }
-    }
-    for (hipEvent_t& e : c.dev_ring)
-        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-            e = nullptr;
-            return false;
-        }
-    return true;
-}
-
-// Appends `n` bytes host -> device at dst (piece by piece; returns at once
-// after the last memcpy, the DMA may still run).
-// Every XCD's L2 written back to memory and invalidated (a system-scope
-// release + acquire per workgroup; 256 workgroups reach all 8 XCDs): after the
-// runtime's host->device copies into the reused per-thread buffers and before
-// the device->host copy of results, so that neither side of a copy can meet a
-// line an L2 kept from an earlier call.
-__global__ __launch_bounds__(64) void k_host_release() { __threadfence_system(); }
-
-hipError_t host_visible(hipStream_t s) {
-    hipLaunchKernelGGL(k_host_release, dim3(256), dim3(64), 0, s);
-    return hipGetLastError();
-}
-
-hipError_t h2d(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s) {
-    HostCtx& c = host_ctx();
-    if (!(staging_mode() & 1) || !stage_init(c)) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s);
-    static thread_local int nb = 0;
-    for (size_t off = 0; off < n; off += kStagePiece) {
-        const size_t len = std::min(kStagePiece, n - off);
-        const int b = nb;
-        nb ^= 1;
-        if (c.pending[b] && wait_ev(c.ev[b], s) != hipSuccess) return hipErrorUnknown;
-        memcpy(c.pin[b], src + off, len);
-        hipError_t e = hipMemcpyAsync(dst + off, c.pin[b], len, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipEventRecord(c.ev[b], s);
-        if (e != hipSuccess) return e;
-        c.pending[b] = true;
-    }
-    return hipSuccess;
-}
-
-// n bytes device -> host, completed on return (the DMA of piece i+1 overlaps
-// the host memcpy of piece i).
-hipError_t d2h(uint8_t* dst, const uint8_t* src, size_t n, hipStream_t s) {
-    HostCtx& c = host_ctx();
-    if (!(staging_mode() & 2) || !stage_init(c)) {
-        const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
-        return e == hipSuccess ? hipStreamSynchronize(s) : e;
-    }
-    for (int b = 0; b < 2; b++)
-        if (c.pending[b] && wait_ev(c.ev[b], s) != hipSuccess) return hipErrorUnknown;
-    c.pending[0] = c.pending[1] = false;
-    const size_t npieces = (n + kStagePiece - 1) / kStagePiece;
-    hipEvent_t done[2] = {nullptr, nullptr};
-    auto issue = [&](size_t i) -> hipError_t {
-        const size_t off = i * kStagePiece, len = std::min(kStagePiece, n - off);
-        done[i & 1] = c.dev_ring[c.ring_pos++ % 8];
-        hipError_t e = hipMemcpyAsync(c.pin[i & 1], src + off, len, hipMemcpyDeviceToHost, s);
-        return e == hipSuccess ? hipEventRecord(done[i & 1], s) : e;
-    };
-    if (npieces && issue(0) != hipSuccess) return hipErrorUnknown;
-    for (size_t i = 0; i < npieces; i++) {
-        if (i + 1 < npieces && issue(i + 1) != hipSuccess) return hipErrorUnknown;
-        if (wait_ev(done[i & 1], s) != hipSuccess) return hipErrorUnknown;
-        const size_t off = i * kStagePiece, len = std::min(kStagePiece, n - off);
-        memcpy(dst + off, c.pin[i & 1], len);
-    }
-    return hipSuccess;
-}
-
-}  // namespace
-
-extern "C" {
-
-static int64_t transpose_host(const void* in, void* out, size_t size, size_t elem_size,
-                              size_t block_size, bool fwd) {
-    Plan p;
-    const int64_t r = make_plan(size, elem_size, block_size, p);
-    if (r) return r;
-    if (!have_device()) return kErrHip;
-    const size_t bytes = size * elem_size;
-    if (bytes == 0) return 0;
-    hipStream_t s = thread_stream();
-    void* di = ctx_buf(HostCtx::kIn, bytes, s);
-    void* dout = ctx_buf(HostCtx::kOut, bytes, s);
-    if (!di || !dout) return -1;
-    if (h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess || host_visible(s) != hipSuccess)
-        return kErrHip;
-    const int64_t n = transpose_dev(di, dout, size, elem_size, block_size, s, fwd);
-    if (n < 0) return n;
-    if (host_visible(s) != hipSuccess || d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess)
-        return kErrHip;
-    return n;
-}
-
-int64_t bshuf_bitshuffle(const void* in, void* out, const size_t size, const size_t elem_size,
-                         size_t block_size) {
-    return transpose_host(in, out, size, elem_size, block_size, true);
-}
-
-int64_t bshuf_bitunshuffle(const void* in, void* out, const size_t size, const size_t elem_size,
-                           size_t block_size) {
-    return transpose_host(in, out, size, elem_size, block_size, false);
-}
-
-int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const size_t elem_size,
-                           size_t block_size) {
-    Plan p;
-    const int64_t r = make_plan(size, elem_size, block_size, p);
-    if (r) return r;
-    if (!have_device()) return kErrHip;
-    const size_t bytes = size * elem_size;
-    const size_t bound = bshuf_compress_lz4_bound(size, elem_size, block_size);
-    const size_t wsb = bshuf_compress_lz4_dev_workspace(size, elem_size, block_size);
-    hipStream_t s = thread_stream();
-    void* di = ctx_buf(HostCtx::kIn, bytes, s);
-    void* dout = ctx_buf(HostCtx::kOut, bound, s);
-    void* ws = ctx_buf(HostCtx::kWs, wsb, s);
-    int64_t* dres = (int64_t*)ctx_buf(HostCtx::kRes, 8, s);
-    if (!di || !dout || !ws || !dres) return -1;
-    if ((bytes && h2d((uint8_t*)di, (const uint8_t*)in, bytes, s) != hipSuccess) ||
-        host_visible(s) != hipSuccess)
-        return kErrHip;
-    const int64_t e = bshuf_compress_lz4_dev(di, dout, size, elem_size, block_size, ws, wsb, dres,
-                                             nullptr, s);
-    if (e < 0) return e;
-    int64_t res = 0;
-    if (host_visible(s) != hipSuccess ||
-        hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return kErrHip;
-    if (res > 0 && (size_t)res <= bound &&
-        d2h((uint8_t*)out, (const uint8_t*)dout, (size_t)res, s) != hipSuccess)
-        return kErrHip;
-    return res;
-}
-
-int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const size_t elem_size,
-                             size_t block_size) {
-    Plan p;
-    const int64_t r = make_plan(size, elem_size, block_size, p);
-    if (r) return r;
-    if (!have_device()) return kErrHip;
-    const size_t bytes = size * elem_size;
-    hipStream_t s = thread_stream();
-    // The stream is at most the compress bound: stage into a buffer of that
-    // size while the walk below finds its real length.
-    const size_t max_in = bshuf_compress_lz4_bound(size, elem_size, block_size);
-    uint8_t* di = (uint8_t*)ctx_buf(HostCtx::kIn, max_in, s);
-    void* dout = ctx_buf(HostCtx::kOut, bytes, s);
-    uint64_t* doffs = (uint64_t*)ctx_buf(HostCtx::kOffs, (size_t)p.nb * 8, s);
-    int64_t* dres = (int64_t*)ctx_buf(HostCtx::kRes, 8, s);
-    if (!di || !dout || !doffs || !dres) return -1;
-    // Walk the BE32 headers through the host buffer (the reference's own
-    // iochain walk, src/bitshuffle.c:92-95) -- this also tells how many bytes
-    // of `in` belong to the stream, which the caller does not pass.  Every
-    // kStagePiece bytes walked leave for the device at once, so the copy
-    // overlaps the rest of the walk.
-    // The walk stops at the first implausible header (length 0 or above
-    // LZ4_compressBound of its block): that record is staged up to the bound,
-    // the blocks behind it keep the all-ones "unresolved" offset, and the
-    // device decoder assigns every error code (-1001 / -91 / -1YYY), exactly
-    // as bshuf_decompress_lz4_dev does for the same bytes.
-    const uint8_t* i8 = (const uint8_t*)in;
-    std::vector<uint64_t>& offs = host_ctx().offs;
-    offs.assign((size_t)p.nb, ~(uint64_t)0);
-    uint64_t pos = 0, issued = 0;
-    bool broken = false;
-    for (int64_t k = 0; k < p.nb; k++) {
-        offs[(size_t)k] = pos;
-        const uint8_t* h = i8 + pos;
-        const uint32_t len = ((uint32_t)h[0] << 24) | ((uint32_t)h[1] << 16) |
-                             ((uint32_t)h[2] << 8) | h[3];
-        const uint32_t bound = (uint32_t)lz4_bound((k < p.L.nfull ? p.L.bs : p.L.last) * p.L.E);
-        if (len == 0 || len > bound) {
-            pos += 4 + (len ? (uint64_t)bound : 0);
-            broken = true;
-            break;
-        }
-        pos += 4 + (uint64_t)len;
-        if (pos - issued >= kStagePiece) {
-            if (h2d(di + issued, i8 + issued, (size_t)(pos - issued), s) != hipSuccess) return kErrHip;
-            issued = pos;
-        }
-    }
-    const size_t in_nbytes = (size_t)pos + (broken ? 0 : (size_t)p.tail);
-    if (in_nbytes > max_in) return -91;
-    if ((in_nbytes > issued && h2d(di + issued, i8 + issued, in_nbytes - issued, s) != hipSuccess) ||
-        (p.nb && hipMemcpyAsync(doffs, offs.data(), (size_t)p.nb * 8, hipMemcpyHostToDevice, s) !=
-                     hipSuccess) ||
-        host_visible(s) != hipSuccess)
-        return kErrHip;
-    // the thread's cached workspace (no stream-ordered allocation per call)
-    const size_t wsb = bshuf_decompress_lz4_dev_workspace(in_nbytes, size, elem_size, block_size);
-    void* ws = ctx_buf(HostCtx::kWs, wsb, s);
-    if (!ws) return -1;
-    const int64_t e = bshuf_decompress_lz4_dev(di, in_nbytes, dout, size, elem_size, block_size,
-                                               ws, wsb, dres, doffs, s);
-    if (e < 0) return e;
-    int64_t res = 0;
-    if (host_visible(s) != hipSuccess ||
-        hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return kErrHip;
-    if (res >= 0 && bytes && d2h((uint8_t*)out, (const uint8_t*)dout, bytes, s) != hipSuccess)
-        return kErrHip;
-    return res;
 }
 
 }  // extern "C"

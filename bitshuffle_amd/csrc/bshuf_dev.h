@@ -101,13 +101,6 @@ __device__ __forceinline__ const gbl128c* g128_aligned_down(const void* p) {
     return (const gbl128c*)((uintptr_t)p & ~(uintptr_t)15);
 }
 
-// End of a stream's LAST kernel (the finishers write the tail and the result):
-// a system-scope release writes the XCD's L2 back to memory.  Without it a
-// device->host copy queued right behind the kernel was seen to read the
-// previous contents of the tail's lines now and then (HDF5 regression chunks:
-// the last <= 30 bytes stale, 2-5 in 40 runs of 42 datasets, ROCm 7.2).
-__device__ __forceinline__ void finish_visible() { __threadfence_system(); }
-
 __device__ __forceinline__ uint32_t lds_rd32(const lds8* D, int p) {
     const lds32* w = (const lds32*)(D + (p & ~3));
     return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(p & 3));

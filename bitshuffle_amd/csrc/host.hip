@@ -1,0 +1,642 @@
+// host.hip -- the host-pointer drop-in entry points: bshuf_bitshuffle /
+// bshuf_bitunshuffle (src/bitshuffle_core.c:2049-2062) and bshuf_compress_lz4 /
+// bshuf_decompress_lz4 (src/bitshuffle.c:236-247), over the device kernels.
+//
+// Every calling thread owns one HIP stream, grow-only device buffers and two
+// pinned staging slots; all of it is released when the thread exits.
+//
+// Transport.  Bytes cross PCIe ONLY through the two kernels of this file,
+// k_xfer<pull> (pinned host slot -> device buffer) and k_xfer<push> (device
+// buffer -> pinned host slot).  They access the pinned, fine-grained slot
+// memory with system-coherent `sc0 sc1` loads and stores, and every workgroup
+// publishes "my part is done" by storing the transfer's sequence number into
+// its own flag word of the slot (behind a system-scope release for push).  The
+// host reuses a slot, or reads the bytes of a pushed piece, only after it has
+// seen EVERY flag word of that piece carry the piece's sequence number -- so no
+// result depends on when a HIP event or stream query reports completion.
+//
+// The DMA engines and the runtime's pinning of pageable caller buffers are not
+// used, so completion never rests on a copy engine's event.  (They were not the
+// cause of the round-2 stale-result defect -- re-mapped stream-ordered pool
+// memory was, DESIGN.md §4.2 -- but the flag protocol makes every host-visible
+// byte's completion checkable.)  BSHUF_HOST_XFER=dma / dma_staged / dma_fenced
+// bring DMA copies back for that experiment only (tools/h5_repro.sh).
+#include <hip/hip_runtime.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+#include <vector>
+
+#include "../../include/bitshuffle.h"
+#include "plan.h"
+
+using namespace bshuf;
+
+namespace {
+
+constexpr size_t kPiece = 8u << 20;   // bytes per staging slot
+constexpr int kXferThreads = 256;
+constexpr int kXferMaxGrid = 256;     // workgroups per piece = flag words per slot
+
+// ---------------------------------------------------------------------------
+// system-coherent global accesses (gfx950 cache policy sc0 sc1: bypass the
+// CU's L1 and the XCD's L2 for this access, whatever the page's memory type)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ld_sys4(const uint8_t* p, int64_t step, u32x4& a, u32x4& b, u32x4& c,
+                                        u32x4& d) {
+    const uint8_t *p1 = p + step, *p2 = p + 2 * step, *p3 = p + 3 * step;
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off sc0 sc1\n\t"
+        "global_load_dwordx4 %1, %5, off sc0 sc1\n\t"
+        "global_load_dwordx4 %2, %6, off sc0 sc1\n\t"
+        "global_load_dwordx4 %3, %7, off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+        : "v"(p), "v"(p1), "v"(p2), "v"(p3)
+        : "memory");
+}
+__device__ __forceinline__ u32x4 ld_sys1(const uint8_t* p) {
+    u32x4 a;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(a) : "v"(p) : "memory");
+    return a;
+}
+__device__ __forceinline__ uint32_t ld_sys_u8(const uint8_t* p) {
+    uint32_t a;
+    asm volatile("global_load_ubyte %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(a) : "v"(p) : "memory");
+    return a;
+}
+__device__ __forceinline__ void st_sys(uint8_t* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sys_u8(uint8_t* p, uint32_t v) {
+    asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sys_u32(uint32_t* p, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+struct XferArgs {
+    uint8_t* dst;         // 16-aligned
+    const uint8_t* src;   // 16-aligned
+    int64_t n;
+    uint32_t* flags;      // kXferMaxGrid words in pinned host memory (device view)
+    uint32_t seq;         // this transfer's number, never 0
+};
+
+// kPush = false: src is pinned host memory (sc0 sc1 loads), dst a device buffer.
+// kPush = true:  src is a device buffer, dst pinned host memory (sc0 sc1 stores).
+template <bool kPush>
+__global__ __launch_bounds__(kXferThreads) void k_xfer(XferArgs a) {
+    const int64_t nch = a.n >> 4;
+    const int64_t stride = (int64_t)gridDim.x * kXferThreads;
+    int64_t c = (int64_t)blockIdx.x * kXferThreads + threadIdx.x;
+    const gbl128c* s16 = (const gbl128c*)a.src;
+    gbl128* d16 = (gbl128*)a.dst;
+    for (; c + 3 * stride < nch; c += 4 * stride) {
+        u32x4 v0, v1, v2, v3;
+        if constexpr (kPush) {
+            v0 = s16[c];
+            v1 = s16[c + stride];
+            v2 = s16[c + 2 * stride];
+            v3 = s16[c + 3 * stride];
+            st_sys(a.dst + 16 * c, v0);
+            st_sys(a.dst + 16 * (c + stride), v1);
+            st_sys(a.dst + 16 * (c + 2 * stride), v2);
+            st_sys(a.dst + 16 * (c + 3 * stride), v3);
+        } else {
+            ld_sys4(a.src + 16 * c, 16 * stride, v0, v1, v2, v3);
+            d16[c] = v0;
+            d16[c + stride] = v1;
+            d16[c + 2 * stride] = v2;
+            d16[c + 3 * stride] = v3;
+        }
+    }
+    for (; c < nch; c += stride) {
+        if constexpr (kPush)
+            st_sys(a.dst + 16 * c, s16[c]);
+        else
+            d16[c] = ld_sys1(a.src + 16 * c);
+    }
+    if (blockIdx.x == 0 && (int64_t)threadIdx.x < (a.n & 15)) {
+        const int64_t i = nch * 16 + threadIdx.x;
+        if constexpr (kPush)
+            st_sys_u8(a.dst + i, a.src[i]);
+        else
+            a.dst[i] = (uint8_t)ld_sys_u8(a.src + i);
+    }
+    // publish: every wave's accesses complete, then one lane per workgroup
+    // (behind a system-scope release for the host-bound data) stores the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if constexpr (kPush) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        st_sys_u32(a.flags + blockIdx.x, a.seq);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+// The round-2 mitigation, kept for the DMA experiment only: a system-scope
+// release + acquire per workgroup (256 workgroups, hoping to meet every XCD).
+__global__ __launch_bounds__(64) void k_l2_flush_all() { __threadfence_system(); }
+
+// ---------------------------------------------------------------------------
+// per-thread state
+// ---------------------------------------------------------------------------
+enum class Xfer { kKernel, kDma, kDmaFenced, kDmaStaged };
+
+Xfer xfer_mode() {
+    static int m = -1;
+    if (m < 0) {
+        const char* e = getenv("BSHUF_HOST_XFER");
+        m = 0;
+        if (e && !strcmp(e, "dma")) m = 1;
+        if (e && !strcmp(e, "dma_fenced")) m = 2;
+        if (e && !strcmp(e, "dma_staged")) m = 3;
+    }
+    return (Xfer)m;
+}
+
+std::atomic<uint64_t> g_stat_late{0};    // flags not yet all set when the event said done
+std::atomic<uint64_t> g_stat_pieces{0};  // staged pieces moved
+
+struct HostCtx {
+    enum { kIn, kOut, kWs, kOffs, kRes, kN };
+    hipStream_t s = nullptr;
+    void* buf[kN] = {};
+    size_t cap[kN] = {};
+    std::vector<uint64_t> offs;
+    struct Slot {
+        uint8_t* host = nullptr;  // pinned, fine-grained
+        uint8_t* dev = nullptr;   // its device view
+        hipEvent_t ev = nullptr;
+        uint32_t seq = 0;
+        int nwg = 0;
+        bool busy = false;
+    };
+    Slot slot[2];
+    uint32_t* flags_host = nullptr;  // 2 x kXferMaxGrid words
+    uint32_t* flags_dev = nullptr;
+    int next = 0;
+    bool broken = false;  // a transport wait failed: refuse further work
+
+    ~HostCtx() {
+        if (!s) return;
+        // the runtime may already be gone at process exit: ignore every error
+        (void)hipStreamSynchronize(s);
+        for (void*& p : buf)
+            if (p) (void)hipFree(p);
+        for (Slot& x : slot) {
+            if (x.host) (void)hipHostFree(x.host);
+            if (x.ev) (void)hipEventDestroy(x.ev);
+        }
+        if (flags_host) (void)hipHostFree(flags_host);
+        (void)hipStreamDestroy(s);
+    }
+
+    bool init() {
+        if (s) return true;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            s = nullptr;
+            return false;
+        }
+        const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+        void* f = nullptr;
+        if (hipHostMalloc(&f, 2 * kXferMaxGrid * sizeof(uint32_t), fl) != hipSuccess) return false;
+        flags_host = (uint32_t*)f;
+        memset(flags_host, 0, 2 * kXferMaxGrid * sizeof(uint32_t));
+        void* fd = nullptr;
+        if (hipHostGetDevicePointer(&fd, f, 0) != hipSuccess) return false;
+        flags_dev = (uint32_t*)fd;
+        for (Slot& x : slot) {
+            void* h = nullptr;
+            if (hipHostMalloc(&h, kPiece + 64, fl) != hipSuccess) return false;
+            x.host = (uint8_t*)h;
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return false;
+            x.dev = (uint8_t*)d;
+            if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) return false;
+        }
+        return true;
+    }
+
+    void* dbuf(int i, size_t n) {
+        if (n == 0) n = 1;
+        if (buf[i] && cap[i] >= n) return buf[i];
+        if (buf[i]) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(buf[i]);
+            buf[i] = nullptr;
+            cap[i] = 0;
+        }
+        const size_t want = std::max(n, cap[i] + cap[i] / 4);
+        if (hipMalloc(&buf[i], want) != hipSuccess) {
+            buf[i] = nullptr;
+            return nullptr;
+        }
+        cap[i] = want;
+        return buf[i];
+    }
+
+    // Waits until every workgroup of the slot's last transfer stored its flag
+    // (after the event of the kernel reported completion).
+    bool settle(int k) {
+        Slot& x = slot[k];
+        if (!x.busy) return true;
+        if (hipEventSynchronize(x.ev) != hipSuccess) return false;
+        volatile uint32_t* f = flags_host + k * kXferMaxGrid;
+        auto all_set = [&]() {
+            for (int w = 0; w < x.nwg; w++)
+                if (f[w] != x.seq) return false;
+            return true;
+        };
+        if (!all_set()) {
+            g_stat_late.fetch_add(1, std::memory_order_relaxed);
+            const time_t t0 = time(nullptr);
+            while (!all_set()) {
+                if (time(nullptr) - t0 > 30) {
+                    fprintf(stderr, "bitshuffle_mi355x: staging transfer never completed\n");
+                    return false;
+                }
+                sched_yield();
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        x.busy = false;
+        return true;
+    }
+
+    // Enqueues one piece through slot k (n <= kPiece; both ends 16-aligned).
+    bool launch(int k, bool push, uint8_t* dst, const uint8_t* src, size_t n) {
+        Slot& x = slot[k];
+        x.seq = x.seq + 1 == 0 ? 1 : x.seq + 1;
+        const int64_t chunks = (int64_t)(n + 15) / 16;
+        x.nwg = (int)std::max<int64_t>(1, std::min<int64_t>(kXferMaxGrid, (chunks + kXferThreads * 4 - 1) /
+                                                                             (kXferThreads * 4)));
+        XferArgs a{dst, src, (int64_t)n, flags_dev + k * kXferMaxGrid, x.seq};
+        if (push)
+            hipLaunchKernelGGL(k_xfer<true>, dim3(x.nwg), dim3(kXferThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_xfer<false>, dim3(x.nwg), dim3(kXferThreads), 0, s, a);
+        if (hipGetLastError() != hipSuccess || hipEventRecord(x.ev, s) != hipSuccess) return false;
+        x.busy = true;
+        g_stat_pieces.fetch_add(1, std::memory_order_relaxed);
+        return true;
+    }
+};
+
+thread_local HostCtx t_ctx;
+
+HostCtx* host_ctx() {
+    if (t_ctx.broken || !t_ctx.init()) return nullptr;
+    return &t_ctx;
+}
+
+hipError_t dma_fence(HostCtx& c) {
+    if (xfer_mode() != Xfer::kDmaFenced) return hipSuccess;
+    hipLaunchKernelGGL(k_l2_flush_all, dim3(256), dim3(64), 0, c.s);
+    return hipGetLastError();
+}
+
+// Round-2 staged DMA transport (diagnostic mode dma_staged): SDMA copies
+// between the device buffers and the pinned slots, completion by HIP events.
+// After each device->host piece is copied out of its slot, the slot is
+// compared with what was copied: a difference means the DMA was still writing
+// the slot after its event reported completion (counted as "late").
+bool h2d_staged(HostCtx& c, uint8_t* dst, const uint8_t* src, uint64_t lo, uint64_t hi) {
+    for (uint64_t off = lo; off < hi; off += kPiece) {
+        const size_t len = (size_t)std::min<uint64_t>(kPiece, hi - off);
+        const int k = c.next;
+        c.next ^= 1;
+        HostCtx::Slot& x = c.slot[k];
+        if (x.busy && hipEventSynchronize(x.ev) != hipSuccess) return false;
+        memcpy(x.host, src + off, len);
+        if (hipMemcpyAsync(dst + off, x.host, len, hipMemcpyHostToDevice, c.s) != hipSuccess ||
+            hipEventRecord(x.ev, c.s) != hipSuccess)
+            return false;
+        x.busy = true;
+    }
+    return true;
+}
+
+bool d2h_staged(HostCtx& c, uint8_t* dst, const uint8_t* src, size_t n) {
+    for (auto& x : c.slot)
+        if (x.busy && hipEventSynchronize(x.ev) != hipSuccess) return false;
+    const size_t np = (n + kPiece - 1) / kPiece;
+    auto issue = [&](size_t i) {
+        const size_t off = i * kPiece, len = std::min(kPiece, n - off);
+        HostCtx::Slot& x = c.slot[i & 1];
+        x.busy = true;
+        return hipMemcpyAsync(x.host, src + off, len, hipMemcpyDeviceToHost, c.s) == hipSuccess &&
+               hipEventRecord(x.ev, c.s) == hipSuccess;
+    };
+    if (!issue(0)) return false;
+    for (size_t i = 0; i < np; i++) {
+        if (i + 1 < np && !issue(i + 1)) return false;
+        HostCtx::Slot& x = c.slot[i & 1];
+        if (hipEventSynchronize(x.ev) != hipSuccess) return false;
+        x.busy = false;
+        const size_t off = i * kPiece, len = std::min(kPiece, n - off);
+        memcpy(dst + off, x.host, len);
+        if (memcmp(dst + off, x.host, len) != 0) g_stat_late.fetch_add(1, std::memory_order_relaxed);
+    }
+    return true;
+}
+
+// Host bytes [lo, hi) of `src` to the device buffer `dst` (same offsets).
+// Returns once the last piece is enqueued; its slot is released later.
+bool h2d(HostCtx& c, uint8_t* dst, const uint8_t* src, uint64_t lo, uint64_t hi) {
+    if (hi <= lo) return true;
+    if (xfer_mode() == Xfer::kDmaStaged) return h2d_staged(c, dst, src, lo, hi);
+    if (xfer_mode() != Xfer::kKernel) {
+        const bool ok = hipMemcpyAsync(dst + lo, src + lo, hi - lo, hipMemcpyHostToDevice, c.s) == hipSuccess;
+        return ok && dma_fence(c) == hipSuccess;
+    }
+    lo &= ~(uint64_t)15;  // re-sending bytes already sent is harmless; keeps both ends aligned
+    for (uint64_t off = lo; off < hi; off += kPiece) {
+        const size_t len = (size_t)std::min<uint64_t>(kPiece, hi - off);
+        const int k = c.next;
+        c.next ^= 1;
+        if (!c.settle(k)) return false;
+        memcpy(c.slot[k].host, src + off, len);
+        if (!c.launch(k, false, dst + off, c.slot[k].dev, len)) return false;
+    }
+    return true;
+}
+
+// n device bytes at `src` (16-aligned) to host `dst`; complete on return.
+bool d2h(HostCtx& c, uint8_t* dst, const uint8_t* src, size_t n) {
+    if (n == 0) return true;
+    if (xfer_mode() == Xfer::kDmaStaged) return d2h_staged(c, dst, src, n);
+    if (xfer_mode() != Xfer::kKernel) {
+        if (dma_fence(c) != hipSuccess) return false;
+        return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c.s) == hipSuccess &&
+               hipStreamSynchronize(c.s) == hipSuccess;
+    }
+    if (!c.settle(0) || !c.settle(1)) return false;
+    const size_t np = (n + kPiece - 1) / kPiece;
+    auto issue = [&](size_t i) {
+        const size_t off = i * kPiece, len = std::min(kPiece, n - off);
+        return c.launch((int)(i & 1), true, c.slot[i & 1].dev, src + off, len);
+    };
+    if (!issue(0)) return false;
+    for (size_t i = 0; i < np; i++) {
+        if (i + 1 < np && !issue(i + 1)) return false;
+        if (!c.settle((int)(i & 1))) return false;
+        const size_t off = i * kPiece, len = std::min(kPiece, n - off);
+        memcpy(dst + off, c.slot[i & 1].host, len);
+    }
+    return true;
+}
+
+// The 8-byte device result word of the stream's last kernel.
+bool read_result(HostCtx& c, const int64_t* dres, int64_t& res) {
+    if (xfer_mode() != Xfer::kKernel) {
+        if (dma_fence(c) != hipSuccess) return false;
+        return hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, c.s) == hipSuccess &&
+               hipStreamSynchronize(c.s) == hipSuccess;
+    }
+    return d2h(c, (uint8_t*)&res, (const uint8_t*)dres, 8);
+}
+
+// Stale-result experiment only (BSHUF_DIAG_WS=alloc): the round-2 host path's
+// per-call stream-ordered workspace (api.hip's DevBuf) instead of the thread's
+// cached one; with BSHUF_DIAG_POOL=default it comes from the default pool.
+bool diag_alloc_ws() {
+    static const bool on = getenv("BSHUF_DIAG_WS") != nullptr;
+    return on;
+}
+
+int64_t fail(HostCtx& c) {
+    c.broken = true;  // a lost transfer may still land later: never reuse these buffers
+    return kErrHip;
+}
+
+int64_t transpose_host(const void* in, void* out, size_t size, size_t elem_size, size_t block_size,
+                       bool fwd) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    const size_t bytes = size * elem_size;
+    if (bytes == 0) return 0;
+    HostCtx* c = host_ctx();
+    if (!c) return kErrHip;
+    uint8_t* di = (uint8_t*)c->dbuf(HostCtx::kIn, bytes);
+    uint8_t* dout = (uint8_t*)c->dbuf(HostCtx::kOut, bytes);
+    if (!di || !dout) return -1;
+    if (!h2d(*c, di, (const uint8_t*)in, 0, bytes)) return fail(*c);
+    const int64_t n = fwd ? bshuf_bitshuffle_dev(di, dout, size, elem_size, block_size, c->s)
+                          : bshuf_bitunshuffle_dev(di, dout, size, elem_size, block_size, c->s);
+    if (n < 0) return n;
+    if (!d2h(*c, (uint8_t*)out, dout, bytes)) return fail(*c);
+    return n;
+}
+
+// Per-thread pinned buffer of stage_upload (the batch segment tables).
+struct TableStage {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    uint32_t* flags_host = nullptr;
+    uint32_t* flags_dev = nullptr;
+    uint32_t seq = 0;
+    int nwg = 0;
+    ~TableStage() {
+        if (host) (void)hipHostFree(host);
+        if (flags_host) (void)hipHostFree(flags_host);
+    }
+    // the previous upload's kernel has read the buffer (its flags are set)
+    bool settle() {
+        if (!nwg) return true;
+        volatile uint32_t* f = flags_host;
+        const time_t t0 = time(nullptr);
+        for (int w = 0; w < nwg;) {
+            if (f[w] == seq) {
+                w++;
+                continue;
+            }
+            if (time(nullptr) - t0 > 30) return false;
+            sched_yield();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        nwg = 0;
+        return true;
+    }
+};
+thread_local TableStage t_table;
+
+}  // namespace
+
+namespace bshuf {
+
+hipError_t stage_upload(const void* host, size_t bytes, void* dev, hipStream_t s) {
+    TableStage& t = t_table;
+    if (!t.settle()) return hipErrorUnknown;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    if (!t.flags_host) {
+        void* f = nullptr;
+        if (hipHostMalloc(&f, kXferMaxGrid * sizeof(uint32_t), fl) != hipSuccess) return hipErrorOutOfMemory;
+        t.flags_host = (uint32_t*)f;
+        memset(f, 0, kXferMaxGrid * sizeof(uint32_t));
+        void* fd = nullptr;
+        if (hipHostGetDevicePointer(&fd, f, 0) != hipSuccess) return hipErrorUnknown;
+        t.flags_dev = (uint32_t*)fd;
+    }
+    if (t.cap < bytes) {
+        if (t.host) (void)hipHostFree(t.host);
+        t.host = t.dev = nullptr;
+        t.cap = 0;
+        void* h = nullptr;
+        if (hipHostMalloc(&h, bytes + 64, fl) != hipSuccess) return hipErrorOutOfMemory;
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return hipErrorUnknown;
+        t.host = (uint8_t*)h;
+        t.dev = (uint8_t*)d;
+        t.cap = bytes;
+    }
+    memcpy(t.host, host, bytes);
+    t.seq = t.seq + 1 == 0 ? 1 : t.seq + 1;
+    XferArgs a{(uint8_t*)dev, t.dev, (int64_t)bytes, t.flags_dev, t.seq};
+    hipLaunchKernelGGL(k_xfer<false>, dim3(1), dim3(kXferThreads), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) t.nwg = 1;
+    return e;
+}
+
+}  // namespace bshuf
+
+extern "C" {
+
+int64_t bshuf_bitshuffle(const void* in, void* out, const size_t size, const size_t elem_size,
+                         size_t block_size) {
+    return transpose_host(in, out, size, elem_size, block_size, true);
+}
+
+int64_t bshuf_bitunshuffle(const void* in, void* out, const size_t size, const size_t elem_size,
+                           size_t block_size) {
+    return transpose_host(in, out, size, elem_size, block_size, false);
+}
+
+int64_t bshuf_compress_lz4(const void* in, void* out, const size_t size, const size_t elem_size,
+                           size_t block_size) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    HostCtx* c = host_ctx();
+    if (!c) return kErrHip;
+    const size_t bytes = size * elem_size;
+    const size_t bound = bshuf_compress_lz4_bound(size, elem_size, block_size);
+    const size_t wsb = bshuf_compress_lz4_dev_workspace(size, elem_size, block_size);
+    uint8_t* di = (uint8_t*)c->dbuf(HostCtx::kIn, bytes);
+    uint8_t* dout = (uint8_t*)c->dbuf(HostCtx::kOut, bound);
+    void* ws = c->dbuf(HostCtx::kWs, wsb);
+    int64_t* dres = (int64_t*)c->dbuf(HostCtx::kRes, 8);
+    if (!di || !dout || !ws || !dres) return -1;
+    if (!h2d(*c, di, (const uint8_t*)in, 0, bytes)) return fail(*c);
+    const bool own = diag_alloc_ws();
+    const int64_t e = bshuf_compress_lz4_dev(di, dout, size, elem_size, block_size, own ? nullptr : ws,
+                                             own ? 0 : wsb, dres, nullptr, c->s);
+    if (e < 0) return e;
+    int64_t res = 0;
+    if (!read_result(*c, dres, res)) return fail(*c);
+    if (res > 0 && (size_t)res <= bound && !d2h(*c, (uint8_t*)out, dout, (size_t)res)) return fail(*c);
+    return res;
+}
+
+int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size, const size_t elem_size,
+                             size_t block_size) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!have_device()) return kErrHip;
+    HostCtx* c = host_ctx();
+    if (!c) return kErrHip;
+    const size_t bytes = size * elem_size;
+    // the stream is at most the compress bound: stage into a buffer of that
+    // size while the walk below finds its real length
+    const size_t max_in = bshuf_compress_lz4_bound(size, elem_size, block_size);
+    uint8_t* di = (uint8_t*)c->dbuf(HostCtx::kIn, max_in);
+    uint8_t* dout = (uint8_t*)c->dbuf(HostCtx::kOut, bytes);
+    uint64_t* doffs = (uint64_t*)c->dbuf(HostCtx::kOffs, (size_t)p.nb * 8);
+    int64_t* dres = (int64_t*)c->dbuf(HostCtx::kRes, 8);
+    if (!di || !dout || !doffs || !dres) return -1;
+    // Walk the BE32 headers through the host buffer (the reference's own
+    // iochain walk, src/bitshuffle.c:92-95): it finds the block offsets and how
+    // many bytes of `in` belong to the stream, which the caller does not pass.
+    // Every kPiece bytes walked leave for the device at once, so the copy
+    // overlaps the rest of the walk.  The walk stops at the first implausible
+    // header (length 0 or above LZ4_compressBound of its block): that block
+    // and every one behind it keep the all-ones "unresolved" offset and
+    // nothing from that header on is staged, so the device decoder reports
+    // -1001 -- as bshuf_decompress_lz4_dev's parallel index rebuild does for
+    // the same bytes.  No byte past the last plausible record is read.
+    const uint8_t* i8 = (const uint8_t*)in;
+    std::vector<uint64_t>& offs = c->offs;
+    offs.assign((size_t)p.nb, ~(uint64_t)0);
+    uint64_t pos = 0, issued = 0;
+    bool broken = false;
+    for (int64_t k = 0; k < p.nb; k++) {
+        const uint8_t* h = i8 + pos;
+        const uint32_t len = ((uint32_t)h[0] << 24) | ((uint32_t)h[1] << 16) |
+                             ((uint32_t)h[2] << 8) | h[3];
+        const uint32_t bound = (uint32_t)lz4_bound((k < p.L.nfull ? p.L.bs : p.L.last) * p.L.E);
+        if (len == 0 || len > bound) {
+            broken = true;
+            break;
+        }
+        offs[(size_t)k] = pos;
+        pos += 4 + (uint64_t)len;
+        if (pos - issued >= kPiece) {
+            if (!h2d(*c, di, i8, issued, pos)) return fail(*c);
+            issued = pos;
+        }
+    }
+    const size_t in_nbytes = (size_t)pos + (broken ? 0 : (size_t)p.tail);
+    if (in_nbytes > max_in) return -91;
+    if (!h2d(*c, di, i8, issued, in_nbytes) ||
+        !h2d(*c, (uint8_t*)doffs, (const uint8_t*)offs.data(), 0, (uint64_t)p.nb * 8))
+        return fail(*c);
+    const size_t wsb = bshuf_decompress_lz4_dev_workspace(in_nbytes, size, elem_size, block_size);
+    void* ws = c->dbuf(HostCtx::kWs, wsb);
+    if (!ws) return -1;
+    const bool own = diag_alloc_ws();
+    const int64_t e = bshuf_decompress_lz4_dev(di, in_nbytes, dout, size, elem_size, block_size,
+                                               own ? nullptr : ws, own ? 0 : wsb, dres, doffs, c->s);
+    if (e < 0) return e;
+    int64_t res = 0;
+    if (!read_result(*c, dres, res)) return fail(*c);
+    if (res >= 0 && bytes && !d2h(*c, (uint8_t*)out, dout, bytes)) return fail(*c);
+    return res;
+}
+
+// Test hook: fills every device buffer and pinned staging slot of the CALLING
+// thread with `byte` (a poisoned previous state for the next host call).
+int64_t bshuf_host_poison(int byte) {
+    if (!have_device()) return kErrHip;
+    HostCtx* c = host_ctx();
+    if (!c) return kErrHip;
+    if (!c->settle(0) || !c->settle(1)) return fail(*c);
+    for (int i = 0; i < HostCtx::kN; i++)
+        if (c->buf[i] && dev_fill(c->buf[i], byte, c->cap[i], c->s) != hipSuccess) return kErrHip;
+    if (hipStreamSynchronize(c->s) != hipSuccess) return kErrHip;
+    for (auto& x : c->slot) memset(x.host, byte, kPiece + 64);
+    return 0;
+}
+
+// Transport counters of the process: out[0] staged pieces moved, out[1] times
+// a piece's completion event fired before all of its flag words were set.
+void bshuf_host_xfer_stats(uint64_t* out2) {
+    out2[0] = g_stat_pieces.load();
+    out2[1] = g_stat_late.load();
+}
+
+}  // extern "C"

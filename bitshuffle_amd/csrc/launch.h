@@ -34,6 +34,10 @@ int diag_variant();  // timing ablations (wrong output), diag build only
 int64_t persistent_grid(const void* fn, int threads, size_t lds, int64_t work);
 // hipMemsetAsync's job done by a kernel (prof.hip)
 hipError_t dev_fill(void* p, int v, size_t n, hipStream_t s);
+// Small host table -> device (16-aligned `dev`) on stream s, by a kernel that
+// reads a per-thread pinned buffer (host.hip; no DMA engine).  Returns at once;
+// the pinned buffer is reused only after that kernel's flags say it was read.
+hipError_t stage_upload(const void* host, size_t bytes, void* dev, hipStream_t s);
 
 // One independent framed stream of a batch (bshuf_*_lz4_batch_dev).  All
 // streams of a batch share elem_size and block_size; global block k of the

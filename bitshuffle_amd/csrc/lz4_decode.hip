@@ -645,11 +645,14 @@ __device__ __forceinline__ uint32_t gw_byte(GWin& g, const uint8_t* P, int clen,
 }
 
 // Record header checks shared by both paths: -1001 when the record does not
-// fit the stream, -91 for an impossible length.
+// fit the stream, -91 for an impossible length.  A length above the LZ4 bound
+// is -91 from the header alone, whatever follows it (the host walk stages
+// only such a header, and must get the device API's code for the same bytes).
 __device__ __forceinline__ int header_status(int64_t clen, int64_t avail, bool last, uint32_t maxlen) {
     if (avail < 4 || clen == 0) return -1000 - 1;  // clen 0: LZ4's srcSize == 0 -> -1
-    if (clen < 0 || clen > (int64_t)maxlen || clen + 4 > avail || (!last && clen + 4 != avail))
-        return (clen + 4 > avail) ? -1000 - 1 : -91;
+    if (clen < 0 || clen > (int64_t)maxlen) return -91;
+    if (clen + 4 > avail) return -1000 - 1;
+    if (!last && clen + 4 != avail) return -91;
     return 0;
 }
 
@@ -949,7 +952,6 @@ __global__ __launch_bounds__(256) void k_decode_finish(const int64_t* __restrict
         else
             *result = end + tail;
     }
-    finish_visible();
 }
 
 }  // namespace
@@ -1124,7 +1126,6 @@ __global__ __launch_bounds__(64) void k_decode_finish_batch(const int64_t* __res
     if (ok)
         for (int64_t i = threadIdx.x; i < g.tail; i += blockDim.x) tail_dst[i] = g.in[end + i];
     if (threadIdx.x == 0) *g.result = last_bad >= 0 ? status[last_bad] : (!ok ? -91 : end + g.tail);
-    finish_visible();
 }
 
 }  // namespace

@@ -984,7 +984,6 @@ __global__ void k_encode_finish(const uint64_t* offs, int64_t nblocks, const uin
     const uint64_t end = offs[nblocks];
     for (int i = threadIdx.x; i < tail; i += blockDim.x) out[end + i] = tail_src[i];
     if (threadIdx.x == 0) *result = (int64_t)end + tail;
-    finish_visible();
 }
 
 // Batch: one workgroup per stream.
@@ -995,7 +994,6 @@ __global__ void k_encode_finish_batch(const uint64_t* offs, const Seg* segs, int
     const uint8_t* tail_src = g.in + (g.nfull * (int64_t)bs + g.last) * E;
     for (int i = threadIdx.x; i < g.tail; i += blockDim.x) g.out[end + i] = tail_src[i];
     if (threadIdx.x == 0) *g.result = (int64_t)end + g.tail;
-    finish_visible();
 }
 
 // Device check of the property Table::exchange relies on: same-address lanes

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -63,12 +64,10 @@ static int g_diag_variant = 0;
 int diag_variant() { return g_diag_variant; }
 #endif
 
-// Device memory set by a kernel instead of hipMemsetAsync: a runtime memset
-// queued before a kernel on the same stream was seen not to be what that
-// kernel read now and then (decode's `bad` word holding an old block index:
-// a decoded chunk reported success with its raw tail never copied, ~1 call in
-// 1,000 of the HDF5 regression set, early in a process).  Stores from a kernel
-// reach later kernels through the ordinary kernel-boundary ordering.
+// Device memory set by a kernel (hipMemsetAsync's job).  Round 2 blamed the
+// runtime memset for a stale `bad` word; the round-3 experiment (DESIGN.md
+// §4.2) cleared it -- the runtime memset alone gave 0 wrong results in 40
+// fresh processes -- so this is simply the codec's own fill.
 __global__ __launch_bounds__(256) void k_fill(uint8_t* __restrict__ p, uint32_t v, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

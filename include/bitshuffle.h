@@ -109,6 +109,15 @@ void bshuf_prof_enable(int on);
 int bshuf_set_variant(int v);
 size_t bshuf_prof_collect(char* buf, size_t len);
 
+/* Host-pointer path internals (additive).  bshuf_host_poison fills every
+ * cached device buffer and pinned staging slot of the CALLING thread with
+ * `byte`, so a test can start the next host call from poisoned state.
+ * bshuf_host_xfer_stats: out2[0] = staged pieces moved by the transfer
+ * kernels, out2[1] = pieces whose completion event fired before all of their
+ * flag words were set (the host waited for the flags). */
+int64_t bshuf_host_poison(int byte);
+void bshuf_host_xfer_stats(uint64_t* out2);
+
 #ifdef __cplusplus
 }
 #endif
