@@ -187,6 +187,43 @@ def copy_peak_gbps(dev, nbytes=2 << 30, reps=5):
     return gbps
 
 
+# ------------------------------------------------------------ parity digests
+def load_digests():
+    """SHA-256 digests of the REFERENCE's own output at full BASELINE sizes
+    (tests/golden/vectors.json "full", made by tests/golden/make_vectors.py
+    from oracle/_ref, the reference C compiled from /root/reference)."""
+    p = os.path.join(ROOT, "tests", "golden", "vectors.json")
+    return {v["name"]: v for v in json.load(open(p))["full"]}
+
+
+def sha256_dev(t, nbytes=None):
+    """SHA-256 of the first nbytes of a device tensor, streamed to the host in
+    256 MiB slices (bounded host memory)."""
+    import hashlib
+    import torch
+    u8 = t.reshape(-1).view(torch.uint8)
+    nbytes = u8.numel() if nbytes is None else int(nbytes)
+    h = hashlib.sha256()
+    step = 256 << 20
+    host = torch.empty(min(step, max(nbytes, 1)), dtype=torch.uint8, pin_memory=True)
+    for off in range(0, nbytes, step):
+        n = min(step, nbytes - off)
+        host[:n].copy_(u8[off:off + n])
+        h.update(memoryview(host[:n].numpy()))
+    return h.hexdigest()
+
+
+def check_digests(pairs, world, device):
+    """pairs: [(name, what, got, want)].  Every rank learns whether ANY rank
+    saw a mismatch (max over ranks), and then all of them exit non-zero."""
+    bad = [(n, w, g, x) for n, w, g, x in pairs if g != x]
+    for n, w, g, x in bad:
+        sys.stderr.write("bench.py: PARITY FAILED %s %s: got %s want %s\n" % (n, w, g, x))
+    if max_over_ranks(1.0 if bad else 0.0, world, device) > 0:
+        raise SystemExit(3)
+    return sorted({n for n, _, _, _ in pairs})
+
+
 # ---------------------------------------------------------------- CPU baseline
 def cpu_model():
     try:
@@ -209,70 +246,93 @@ def _omp_threads(n):
 
 
 def cpu_baseline(sample_mib, cfg):
-    """The reference's own C (oracle/_ref: AVX2 + OpenMP build from the
-    reference sources by oracle/Makefile) timed on this host on a bounded
-    sample of the same workload, with 1 thread and with every core of this
-    process's affinity set.  Falls back to our scalar CPU port (1 thread)
-    when _ref is absent."""
+    """The reference's own C (oracle/_ref, compiled from the reference sources
+    by oracle/Makefile) timed on this host on a bounded sample of the same
+    workload: on the job's CPU share (OMP_NUM_THREADS) and on 1 thread.
+      config 1: the reference's SCALAR build (BASELINE configs[0] names the
+                CPU scalar path) is `value`; its AVX2 build rides along;
+      config 4: one reference call per 32 MiB chunk, as a per-chunk caller
+                (the HDF5 filter) would make them;
+      otherwise the AVX2 + OpenMP build (the haswell wheels).
+    Falls back to our scalar CPU port (1 thread) when _ref is absent."""
     import numpy as np
-    from oracle import Oracle, Reference, reference_available
+    from oracle import REF_SCALAR_SO, Oracle, Reference, reference_available
     o = Oracle()
     gen = cfg["gen"]
     es = {0: 4, 1: 2, 2: 4}[gen]
-    n = sample_mib * (1 << 20) // es
-    a = o.gen_g1(n, 0, 12345) if gen == 1 else (o.gen_g2(n, 0, 12345) if gen == 2 else o.gen_g0(n))
     affinity = len(os.sched_getaffinity(0))
     # the box's CPU share: OMP_NUM_THREADS when the environment sets it (the
     # affinity mask may list far more cores than the job may use; 256 OpenMP
     # threads on a 16-core share run ~25x slower than 16)
     share = int(os.environ.get("OMP_NUM_THREADS") or affinity)
+    scalar_so = REF_SCALAR_SO
+    batch = cfg["what"] == "batch"
+    if batch:
+        cn = cfg["chunk_mib"] * (1 << 20) // es
+        k = max(1, sample_mib // cfg["chunk_mib"])
+        chunks = [o.gen_g1(cn, 0, 12345 + i) for i in range(k)]
+        a = None
+    else:
+        n = sample_mib * (1 << 20) // es
+        a = o.gen_g1(n, 0, 12345) if gen == 1 else (o.gen_g2(n, 0, 12345) if gen == 2 else o.gen_g0(n))
     if reference_available():
-        codec, kind = Reference(), "reference"
+        kind = "reference"
+        codec = Reference(scalar_so) if cfg["what"] == "shuffle" and os.path.exists(scalar_so) \
+            else Reference()
     else:
         codec, kind = o, "port"
 
-    def rate(arr, budget_s):
+    def one_pass(c, arr):
+        if cfg["what"] == "shuffle":
+            return c.bitunshuffle(c.bitshuffle(arr))
+        return c.decompress_lz4(c.compress_lz4(arr), arr.shape, arr.dtype)
+
+    def rate(c, arrs, budget_s):
         best, reps, t_all = None, 0, time.perf_counter()
+        nbytes = sum(x.nbytes for x in arrs)
         while reps < 2 or (time.perf_counter() - t_all < budget_s and reps < 20):
             t0 = time.perf_counter()
-            if cfg["what"] == "shuffle":
-                s = codec.bitshuffle(arr)
-                t1 = time.perf_counter()
-                d = codec.bitunshuffle(s)
-            else:
-                c = codec.compress_lz4(arr)
-                t1 = time.perf_counter()
-                d = codec.decompress_lz4(c, arr.shape, arr.dtype)
+            outs = [one_pass(c, x) for x in arrs]
             t2 = time.perf_counter()
             if reps == 0:
-                assert np.array_equal(d, arr)
-            v = arr.nbytes / (t2 - t0) / GIB
+                assert all(np.array_equal(d, x) for d, x in zip(outs, arrs))
+            v = nbytes / (t2 - t0) / GIB
             best = v if best is None else max(best, v)
             reps += 1
         return best, reps
 
+    arrs = chunks if batch else [a]
     res = {"unit": "GiB/s", "kind": kind, "cpu_model": cpu_model(), "affinity_cores": affinity,
            "os_cpu_count": os.cpu_count()}
+    what = {"shuffle": "bitshuffle+bitunshuffle", "lz4": "bitshuffle+LZ4 compress + decompress",
+            "batch": "bitshuffle+LZ4 compress + decompress, one call per 32 MiB chunk"}[cfg["what"]]
+    total_mib = sum(x.nbytes for x in arrs) >> 20
     if kind == "reference":
         _omp_threads(share)
-        v_all, reps_all = rate(a, 8.0)
-        one = a[: max(len(a) // 8, 1 << 16)]
+        v_all, reps_all = rate(codec, arrs, 8.0)
+        one = arrs[:1] if batch else [a[: max(len(a) // 8, 1 << 16)]]
         _omp_threads(1)
-        v_one, reps_one = rate(one, 6.0)
+        v_one, reps_one = rate(codec, one, 6.0)
         _omp_threads(share)
+        build = "SCALAR build (-mno-sse2 -mno-avx -mno-avx2)" if codec.path == scalar_so \
+            else "-march=haswell (AVX2) build"
         res.update(value=round(v_all, 3), cores=share, value_1thread=round(v_one, 3),
-                   sample="%d MiB %s (seed 12345) on the job's CPU share (OMP_NUM_THREADS), best of %d; %d MiB 1-thread, best "
-                          "of %d; %s round trip through the reference C-ABI, compiled from "
-                          "/root/reference -O3 -march=haswell -fopenmp (setup.py flags)" % (
-                              a.nbytes >> 20, cfg["dtype"], reps_all, one.nbytes >> 20, reps_one,
-                              "bitshuffle+bitunshuffle" if cfg["what"] == "shuffle"
-                              else "bitshuffle+LZ4 compress + decompress"))
+                   sample="%d MiB %s (seed 12345) on the job's CPU share (OMP_NUM_THREADS), best of %d; "
+                          "%d MiB 1-thread, best of %d; %s round trip through the reference C-ABI, "
+                          "compiled from /root/reference -O3 -fopenmp (setup.py flags), %s" % (
+                              total_mib, cfg["dtype"], reps_all, sum(x.nbytes for x in one) >> 20,
+                              reps_one, what, build))
+        if cfg["what"] == "shuffle" and codec.path == scalar_so:
+            avx = Reference()
+            _omp_threads(share)
+            v_avx, _ = rate(avx, arrs, 4.0)
+            res["value_avx2_build"] = round(v_avx, 3)
     else:
-        one = a[: min(len(a), 1 << 24)]
-        v_one, reps_one = rate(one, 8.0)
+        one = arrs[:1] if batch else [a[: min(len(a), 1 << 24)]]
+        v_one, reps_one = rate(o, one, 8.0)
         res.update(value=round(v_one, 3), cores=1, value_1thread=round(v_one, 3),
                    sample="%d MiB, scalar oracle port, 1 thread, best of %d" % (
-                       one.nbytes >> 20, reps_one))
+                       sum(x.nbytes for x in one) >> 20, reps_one))
     return res
 
 
@@ -311,6 +371,7 @@ def main(argv=None):
             _, res = api.compress_lz4_batch_dev(xs, outs=outs, sync=False)
             counts = res.cpu().tolist()  # the decoder needs the stream lengths
             state["C"] = sum(counts)
+            state["counts"] = counts
             api.decompress_lz4_batch_dev([o[:c] for o, c in zip(outs, counts)],
                                          [x.shape for x in xs], dt, outs=ys, sync=False)
 
@@ -365,11 +426,37 @@ def main(argv=None):
                         gib, cfg["dtype"], "G1 correlated noise" if cfg["gen"] == 1
                         else "G2 smooth field", B.default_block_size(es)))
 
-    # parity gate before timing: exact round trip
+    # parity gate before timing: exact round trip, and on every rank that owns
+    # a BASELINE input with a committed reference digest, the input and the
+    # framed stream byte-for-byte against the REFERENCE's output (length +
+    # SHA-256).  Any mismatch exits non-zero before anything is timed.
     step()
     torch.cuda.synchronize()
     if not check():
         raise SystemExit("round trip parity FAILED on rank %d" % rank)
+    digests, pairs = load_digests(), []
+    if cfg["what"] == "shuffle" and rank == 0 and gib == cfg["gib"]:
+        d = digests["cfg1_g0_i32_64MiB"]
+        pairs += [(d["name"], "input_sha256", sha256_dev(x), d["input_sha256"]),
+                  (d["name"], "shuffled_sha256", sha256_dev(s_buf), d["shuffled_sha256"])]
+    elif cfg["what"] == "lz4" and rank == 0 and gib == cfg["gib"]:
+        d = digests["cfg2_g1_i16_4GiB" if args.config == 2 else "cfg3_g2_f32_16GiB"]
+        pairs += [(d["name"], "input_sha256", sha256_dev(x), d["input_sha256"]),
+                  (d["name"], "compressed_len", state["C"], d["compressed_len"]),
+                  (d["name"], "compressed_sha256", sha256_dev(comp, state["C"]),
+                   d["compressed_sha256"])]
+    elif cfg["what"] == "batch" and cfg["chunk_mib"] == 32:
+        for i in range(nchunks):
+            name = "cfg4_g1_chunk%04d" % (rank * nchunks + i)
+            if name in digests:
+                d = digests[name]
+                c = state["counts"][i]
+                pairs += [(name, "compressed_len", c, d["compressed_len"]),
+                          (name, "compressed_sha256", sha256_dev(outs[i], c), d["compressed_sha256"])]
+    checked = check_digests(pairs, world, dev)
+    parity = {"kind": "reference-digest" if checked else "self-round-trip",
+              "round_trip_exact": True, "digests_matched": checked,
+              "source": "tests/golden/vectors.json (reference C output, SHA-256 + length)"}
 
     if not args.no_prof:
         lib.bshuf_prof_enable(1)
@@ -440,7 +527,7 @@ def main(argv=None):
                        "ratio": round(nbytes / C, 4) if C else None,
                        "parallelism": "shard-per-gpu x%d" % world},
             "roofline": roofline, "round_trip": stage, "kernels_avg_ms": kernels,
-            "cpu_baseline": cpu,
+            "parity": parity, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -44,6 +44,22 @@ PROTOTYPES = {
     "bshuf_set_variant": (_int, [_int]),
     "bshuf_prof_collect": (_sz, [ctypes.c_char_p, _sz]),
     "bshuf_host_poison": (_i64, [_int]),
+    # include/bitshuffle_internals.h (the reference's Cython hooks)
+    **{n: (_i64, [_vp, _vp, _sz, _sz]) for n in (
+        "bshuf_copy", "bshuf_trans_byte_elem_scal", "bshuf_trans_bit_byte_scal",
+        "bshuf_trans_bitrow_eight", "bshuf_trans_bit_elem_scal", "bshuf_trans_byte_bitrow_scal",
+        "bshuf_shuffle_bit_eightelem_scal", "bshuf_untrans_bit_elem_scal", "bshuf_trans_bit_elem",
+        "bshuf_untrans_bit_elem")},
+    **{"bshuf_%s_%s" % (f, isa): (_i64, [_vp, _vp, _sz, _sz])
+       for isa, fs in (("SSE", ("trans_byte_elem", "trans_bit_byte", "trans_bit_elem",
+                                 "trans_byte_bitrow", "shuffle_bit_eightelem", "untrans_bit_elem")),
+                       ("NEON", ("trans_byte_elem", "trans_bit_byte", "trans_bit_elem",
+                                  "trans_byte_bitrow", "shuffle_bit_eightelem", "untrans_bit_elem")),
+                       ("AVX", ("trans_bit_byte", "trans_bit_elem", "trans_byte_bitrow",
+                                 "shuffle_bit_eightelem", "untrans_bit_elem")),
+                       ("AVX512", ("trans_bit_byte", "trans_bit_elem", "shuffle_bit_eightelem",
+                                    "untrans_bit_elem")))
+       for f in fs},
     "bshuf_host_xfer_stats": (None, [_vp]),
 }
 

@@ -640,3 +640,135 @@ void bshuf_host_xfer_stats(uint64_t* out2) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// The reference's internal transpose steps (include/bitshuffle_internals.h,
+// bitshuffle/ext.pyx:56-86): host pointers in and out, the step itself on the
+// device (internals.hip, or a one-block call of the transpose kernels).
+// ---------------------------------------------------------------------------
+#include "../../include/bitshuffle_internals.h"
+
+namespace {
+
+constexpr int64_t kErrNotMult8 = -80;  // CHECK_MULT_EIGHT, src/bitshuffle_internals.h
+
+template <class Op>
+int64_t host_step(const void* in, void* out, size_t size, size_t elem_size, Op op) {
+    if (!have_device()) return kErrHip;
+    const size_t bytes = size * elem_size;
+    if (bytes == 0) return 0;
+    HostCtx* c = host_ctx();
+    if (!c) return kErrHip;
+    uint8_t* di = (uint8_t*)c->dbuf(HostCtx::kIn, bytes);
+    uint8_t* dout = (uint8_t*)c->dbuf(HostCtx::kOut, bytes);
+    if (!di || !dout) return -1;
+    if (!h2d(*c, di, (const uint8_t*)in, 0, bytes)) return fail(*c);
+    const int64_t r = op(di, dout, c->s);
+    if (r < 0) return r;
+    if (!d2h(*c, (uint8_t*)out, dout, bytes)) return fail(*c);
+    return (int64_t)bytes;
+}
+
+int64_t bit_block(const void* in, void* out, size_t size, size_t elem_size, bool fwd) {
+    if (size % 8) return kErrNotMult8;
+    return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
+        return fwd ? bshuf_bitshuffle_dev(di, dout, size, elem_size, size, s)
+                   : bshuf_bitunshuffle_dev(di, dout, size, elem_size, size, s);
+    });
+}
+
+int64_t trans_elem_step(const void* in, void* out, size_t size, size_t elem_size, int64_t lda,
+                        int64_t ldb, int64_t es) {
+    return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
+        return launch_trans_elem(di, dout, lda, ldb, es, s) == hipSuccess ? 0 : kErrHip;
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t bshuf_copy(const void* in, void* out, const size_t size, const size_t elem_size) {
+    return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
+        return hipMemcpyAsync(dout, di, size * elem_size, hipMemcpyDeviceToDevice, s) == hipSuccess
+                   ? 0 : kErrHip;
+    });
+}
+
+int64_t bshuf_trans_byte_elem_scal(const void* in, void* out, const size_t size, const size_t elem_size) {
+    return trans_elem_step(in, out, size, elem_size, (int64_t)size, (int64_t)elem_size, 1);
+}
+
+int64_t bshuf_trans_bit_byte_scal(const void* in, void* out, const size_t size, const size_t elem_size) {
+    const size_t nbyte = size * elem_size;
+    if (nbyte % 8) return kErrNotMult8;
+    return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
+        return bshuf_bitshuffle_dev(di, dout, nbyte, 1, nbyte, s);
+    });
+}
+
+int64_t bshuf_trans_bitrow_eight(const void* in, void* out, const size_t size, const size_t elem_size) {
+    if (size % 8) return kErrNotMult8;
+    return trans_elem_step(in, out, size, elem_size, 8, (int64_t)elem_size, (int64_t)(size / 8));
+}
+
+int64_t bshuf_trans_bit_elem_scal(const void* in, void* out, const size_t size, const size_t elem_size) {
+    return bit_block(in, out, size, elem_size, true);
+}
+
+int64_t bshuf_trans_byte_bitrow_scal(const void* in, void* out, const size_t size,
+                                     const size_t elem_size) {
+    if (size % 8) return kErrNotMult8;
+    return trans_elem_step(in, out, size, elem_size, 8 * (int64_t)elem_size, (int64_t)(size / 8), 1);
+}
+
+int64_t bshuf_shuffle_bit_eightelem_scal(const void* in, void* out, const size_t size,
+                                         const size_t elem_size) {
+    if (size % 8) return kErrNotMult8;
+    return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
+        return launch_shuffle_bit_eightelem(di, dout, (int64_t)size, (int64_t)elem_size, s) == hipSuccess
+                   ? 0 : kErrHip;
+    });
+}
+
+int64_t bshuf_untrans_bit_elem_scal(const void* in, void* out, const size_t size, const size_t elem_size) {
+    return bit_block(in, out, size, elem_size, false);
+}
+
+int64_t bshuf_trans_bit_elem(const void* in, void* out, const size_t size, const size_t elem_size) {
+    return bit_block(in, out, size, elem_size, true);
+}
+
+int64_t bshuf_untrans_bit_elem(const void* in, void* out, const size_t size, const size_t elem_size) {
+    return bit_block(in, out, size, elem_size, false);
+}
+
+#define BSHUF_MISSING_ISA(name, code)                                                       \
+    int64_t name(const void* in, void* out, const size_t size, const size_t elem_size) {   \
+        (void)in, (void)out, (void)size, (void)elem_size;                                   \
+        return code;                                                                        \
+    }
+BSHUF_MISSING_ISA(bshuf_trans_byte_elem_SSE, -11)
+BSHUF_MISSING_ISA(bshuf_trans_bit_byte_SSE, -11)
+BSHUF_MISSING_ISA(bshuf_trans_bit_elem_SSE, -11)
+BSHUF_MISSING_ISA(bshuf_trans_byte_bitrow_SSE, -11)
+BSHUF_MISSING_ISA(bshuf_shuffle_bit_eightelem_SSE, -11)
+BSHUF_MISSING_ISA(bshuf_untrans_bit_elem_SSE, -11)
+BSHUF_MISSING_ISA(bshuf_trans_bit_byte_AVX, -12)
+BSHUF_MISSING_ISA(bshuf_trans_bit_elem_AVX, -12)
+BSHUF_MISSING_ISA(bshuf_trans_byte_bitrow_AVX, -12)
+BSHUF_MISSING_ISA(bshuf_shuffle_bit_eightelem_AVX, -12)
+BSHUF_MISSING_ISA(bshuf_untrans_bit_elem_AVX, -12)
+BSHUF_MISSING_ISA(bshuf_trans_byte_elem_NEON, -13)
+BSHUF_MISSING_ISA(bshuf_trans_bit_byte_NEON, -13)
+BSHUF_MISSING_ISA(bshuf_trans_bit_elem_NEON, -13)
+BSHUF_MISSING_ISA(bshuf_trans_byte_bitrow_NEON, -13)
+BSHUF_MISSING_ISA(bshuf_shuffle_bit_eightelem_NEON, -13)
+BSHUF_MISSING_ISA(bshuf_untrans_bit_elem_NEON, -13)
+BSHUF_MISSING_ISA(bshuf_trans_bit_byte_AVX512, -14)
+BSHUF_MISSING_ISA(bshuf_trans_bit_elem_AVX512, -14)
+BSHUF_MISSING_ISA(bshuf_shuffle_bit_eightelem_AVX512, -14)
+BSHUF_MISSING_ISA(bshuf_untrans_bit_elem_AVX512, -14)
+#undef BSHUF_MISSING_ISA
+
+}  // extern "C"

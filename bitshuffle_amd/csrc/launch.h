@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "bshuf_dev.h"
 
 namespace bshuf {
@@ -133,6 +135,14 @@ hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_
                               int64_t nchunks, const DecodeBufs& b, hipStream_t s);
 hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
                                const Layout& L, const DecodeBufs& b, hipStream_t s);
+
+// ---- the reference's internal transpose steps (internals.hip) -------------
+// out[(j * lda + i) * es + t] = in[(i * ldb + j) * es + t]  (bshuf_trans_elem)
+hipError_t launch_trans_elem(const uint8_t* in, uint8_t* out, int64_t lda, int64_t ldb, int64_t es,
+                             hipStream_t s);
+// bshuf_shuffle_bit_eightelem_scal of `size` (multiple of 8) E-byte elements
+hipError_t launch_shuffle_bit_eightelem(const uint8_t* in, uint8_t* out, int64_t size, int64_t E,
+                                        hipStream_t s);
 
 // ---- synthetic inputs ----------------------------------------------------
 hipError_t launch_synth(void* out, size_t n, int gen, uint64_t first, uint64_t seed,
