@@ -58,6 +58,10 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--gib", type=float, default=None, help="uncompressed GiB per GPU (override)")
+    ap.add_argument("--elem-size", type=int, default=None,
+                    help="configs 2/3: read the same synthetic bytes as elements of this many bytes")
+    ap.add_argument("--block-size", type=int, default=None,
+                    help="configs 2/3: block size in elements (0 = the reference's default)")
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip per-kernel event timing")
@@ -398,6 +402,53 @@ def main(argv=None):
             return torch.equal(x, y)
         workload = ("bshuf_bitshuffle + bshuf_bitunshuffle of a %.3g MiB %s ramp (G0), default "
                     "blocks, device-resident" % (nbytes / (1 << 20), cfg["dtype"]))
+    elif args.elem_size or args.block_size:
+        # the same synthetic bytes, framed with another element size and/or
+        # block size through the C-ABI directly (no torch dtype of E bytes)
+        E = args.elem_size or es
+        bsz = args.block_size or 0
+        n = int(gib * GIB) // E // 8 * 8
+        nbytes = n * E
+        xs = torch.empty((nbytes + es - 1) // es, dtype=dt, device=dev)
+        B.synth_fill_dev(xs, cfg["gen"], first=0, seed=12345 + rank)
+        x = xs.view(torch.uint8)[:nbytes]
+        bound = int(lib.bshuf_compress_lz4_bound(n, E, bsz))
+        if bound > (1 << 62):
+            raise SystemExit("bench.py: invalid --block-size %d" % bsz)
+        comp = torch.empty(bound, dtype=torch.uint8, device=dev)
+        wse = torch.empty(max(int(lib.bshuf_compress_lz4_dev_workspace(n, E, bsz)), 256),
+                          dtype=torch.uint8, device=dev)
+        wsd = torch.empty(max(int(lib.bshuf_decompress_lz4_dev_workspace(bound, n, E, bsz)), 256),
+                          dtype=torch.uint8, device=dev)
+        res_e = torch.empty(1, dtype=torch.int64, device=dev)
+        res_d = torch.empty(1, dtype=torch.int64, device=dev)
+        y = torch.empty_like(x)
+        state = {}
+        vp = ctypes.c_void_p
+
+        def step():
+            st = vp(torch.cuda.current_stream().cuda_stream)
+            r = lib.bshuf_compress_lz4_dev(vp(x.data_ptr()), vp(comp.data_ptr()), n, E, bsz,
+                                           vp(wse.data_ptr()), wse.numel(), vp(res_e.data_ptr()),
+                                           None, st)
+            if r < 0:
+                raise SystemExit("bshuf_compress_lz4_dev: %d" % r)
+            c = int(res_e.item())
+            state["C"] = c
+            r = lib.bshuf_decompress_lz4_dev(vp(comp.data_ptr()), c, vp(y.data_ptr()), n, E, bsz,
+                                             vp(wsd.data_ptr()), wsd.numel(), vp(res_d.data_ptr()),
+                                             None, st)
+            if r < 0:
+                raise SystemExit("bshuf_decompress_lz4_dev: %d" % r)
+
+        def check():
+            return int(res_d.item()) == state["C"] and torch.equal(x, y)
+        workload = ("bitshuffle+LZ4 encode+decode round trip, %.3g GiB of %s %s bytes per GPU read as "
+                    "%d-byte elements, block size %d elements (%d bytes), device-resident, decoder "
+                    "rebuilds the block index" % (
+                        gib, cfg["dtype"], "G1" if cfg["gen"] == 1 else "G2", E,
+                        bsz or B.default_block_size(E), (bsz or B.default_block_size(E)) * E))
+        es = E
     else:
         n = int(gib * GIB) // es // 8 * 8
         x = torch.empty(n, dtype=dt, device=dev)
@@ -439,7 +490,7 @@ def main(argv=None):
         d = digests["cfg1_g0_i32_64MiB"]
         pairs += [(d["name"], "input_sha256", sha256_dev(x), d["input_sha256"]),
                   (d["name"], "shuffled_sha256", sha256_dev(s_buf), d["shuffled_sha256"])]
-    elif cfg["what"] == "lz4" and rank == 0 and gib == cfg["gib"]:
+    elif cfg["what"] == "lz4" and rank == 0 and gib == cfg["gib"] and not (args.elem_size or args.block_size):
         d = digests["cfg2_g1_i16_4GiB" if args.config == 2 else "cfg3_g2_f32_16GiB"]
         pairs += [(d["name"], "input_sha256", sha256_dev(x), d["input_sha256"]),
                   (d["name"], "compressed_len", state["C"], d["compressed_len"]),
@@ -488,7 +539,11 @@ def main(argv=None):
         traffic = pmc.get(dom) if isinstance(pmc, dict) and args.config == 2 else None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": traffic, "alg_bytes_per_launch": alg.get(dom, nbytes + C),
+                    "traffic": traffic,
+                    "traffic_source": ("profiles/pmc_traffic.json: rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                                       "passes committed for this kernel, not measured in this run"
+                                       if traffic else None),
+                    "alg_bytes_per_launch": alg.get(dom, nbytes + C),
                     "avg_launch_ms": round(avg_s * 1e3, 4)}
         try:
             cp = copy_peak_gbps(dev)
@@ -522,7 +577,7 @@ def main(argv=None):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": workload, "baseline_config": args.config,
-                       "elem_size": es, "block_size": B.default_block_size(es),
+                       "elem_size": es, "block_size": args.block_size or B.default_block_size(es),
                        "bytes_per_gpu": nbytes, "compressed_bytes_rank0": C,
                        "ratio": round(nbytes / C, 4) if C else None,
                        "parallelism": "shard-per-gpu x%d" % world},

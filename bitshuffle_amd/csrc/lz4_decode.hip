@@ -478,6 +478,7 @@ struct DecArgs {
     uint32_t* seq;   // token positions (k_seq_scan -> lz4_exec_block)
     const Seg* segs; // batch: per-stream table (nullptr: the single stream above)
     const uint32_t* blk_seg;
+    int32_t stage_off;  // EK == 0: LDS offset of the output staging block (0: none)
 };
 
 // Where block k lives: its stream's framed bytes, output, token-position area
@@ -897,6 +898,28 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                     }
                     store_group<EK>(dst + (int64_t)g * 8 * EK, w);
                 }
+            } else if (a.stage_off) {
+                // any element size: inverse transpose into an LDS staging
+                // block, then coalesced 8-byte stores (outputs 8-aligned)
+                lds8* S = to_lds(smem) + a.stage_off;
+                const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)E - 1) / (uint64_t)E);
+                for (int i = lane; i < P * E; i += kWave) {
+                    const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                    uint64_t v = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) v |= (uint64_t)D[(8 * b + j) * P + g] << (8 * j);
+                    v = tr8x8(v);
+                    lds8* y = S + 8 * g * E + b;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) y[k * E] = (uint8_t)(v >> (8 * k));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const int nw = P * E;  // 8-byte words of the block
+                for (int i = lane; i < nw; i += kWave) {
+                    const u32x2 v = ((const lds64v*)S)[i];
+                    reinterpret_cast<uint2*>(dst)[i] = make_uint2(v.x, v.y);
+                }
             } else {
                 for (int i = lane; i < P * E; i += kWave) {
                     const int g = i / E, b = i - g * E;
@@ -1062,6 +1085,14 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     const bool touch = grec && tuning_variant() != 32;
     size_t lds = (size_t)a.cap + 16 + (grec ? 0 : rec);
     const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
+    // any other element size: stage the inverse transpose in LDS when every
+    // output is 8-aligned (a.stage_off was set to 1 by the caller as "may")
+    if (ek == 0 && a.stage_off) {
+        a.stage_off = (int32_t)lds;
+        lds += (size_t)a.cap;
+    } else {
+        a.stage_off = 0;
+    }
     const void* fn = nullptr;
 #define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
     switch (ek) {
@@ -1139,7 +1170,8 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr};
+                  (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr,
+                  ((uintptr_t)out & 7) == 0 ? 1 : 0};
         if (nmax > max_lds_decode_bytes()) {
             // large blocks: validated by the same scan, executed in global memory
             e = scan_impl(a, nb, s);
@@ -1164,10 +1196,13 @@ hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
     if (e != hipSuccess) return e;
     if (nb > 0) {
         const int64_t nmax = (int64_t)L.bs * L.E;
+        bool aligned = true, al8 = true;
+        for (int i = 0; i < nsegs; i++) {
+            aligned = aligned && ((uintptr_t)hsegs[i].out & 15) == 0;
+            al8 = al8 && ((uintptr_t)hsegs[i].out & 7) == 0;
+        }
         DecArgs a{nullptr, 0, b.offs, nullptr, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg};
-        bool aligned = true;
-        for (int i = 0; i < nsegs; i++) aligned = aligned && ((uintptr_t)hsegs[i].out & 15) == 0;
+                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg, al8 ? 1 : 0};
         e = decode_impl(a, nb, aligned, s);
         if (e != hipSuccess) return e;
     }

@@ -107,6 +107,7 @@ struct EncArgs {
     int32_t desc_off;
     const Seg* segs;   // batch: per-stream table (nullptr: the single stream in/L)
     const uint32_t* blk_seg;
+    int32_t raw8;      // EK == 0: every block source is 8-aligned (LDS-staged transpose)
 };
 
 // Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
@@ -736,6 +737,31 @@ __device__ __forceinline__ void transpose4_regs_to_lds(const BlockRegs4<EK>& R, 
     }
 }
 
+// Any element size (EK == 0): the block's raw bytes (<= kRawBytes) travel
+// from HBM as coalesced 8-byte loads into registers (prefetched like the
+// EK-specialised paths), land in the still-unused hash-table LDS, and the
+// bit transpose gathers each 8-element group's byte b from there -- the
+// strided byte gathers hit LDS instead of HBM.
+constexpr int kRawBytes = 8192;
+constexpr int kRawIters = kRawBytes / (8 * kWave);
+struct RawRegs {
+    uint2 w[kRawIters];
+};
+__device__ __forceinline__ void issue_raw_loads(RawRegs& R, const uint8_t* src, int nbytes, int lane) {
+#pragma unroll
+    for (int it = 0; it < kRawIters; it++) {
+        const int i = it * kWave + lane;
+        if (8 * i < nbytes) R.w[it] = reinterpret_cast<const uint2*>(src)[i];
+    }
+}
+__device__ __forceinline__ void raw_to_lds(const RawRegs& R, lds8* S, int nbytes, int lane) {
+#pragma unroll
+    for (int it = 0; it < kRawIters; it++) {
+        const int i = it * kWave + lane;
+        if (8 * i < nbytes) ((lds64v*)S)[i] = u32x2{R.w[it].x, R.w[it].y};
+    }
+}
+
 // Persistent: workgroup w handles blocks w, w+G, w+2G, ...  While block k is
 // parsed out of LDS, the 8 KiB of block k+G are already in flight into
 // registers, so HBM latency hides under the (LDS-latency-bound) parse.
@@ -767,6 +793,8 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 
     BlockRegs<EK> R;
     BlockRegs4<EK> R4;
+    RawRegs RW;
+    auto raw_fits = [&](int m) { return EK == 0 && a.raw8 && m * E <= kRawBytes; };
     constexpr bool kX4 = (VAR & 4) == 0;  // 4-groups-per-lane transpose (default)
     // insert/readback search window: the fallback when the device's LDS
     // atomics do not serialise in lane order
@@ -782,6 +810,9 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
             issue_block_loads4<EK>(R4, blk_src(blk), m0 / 8, lane);
         else if (fits(m0))
             issue_block_loads<EK>(R, blk_src(blk), m0 / 8, lane);
+    } else {
+        const int m0 = blk_m(blk);
+        if (raw_fits(m0)) issue_raw_loads(RW, blk_src(blk), m0 * E, lane);
     }
 
     KDIAG_DECL
@@ -791,12 +822,39 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         const int n = m * E;
         const int P = m / 8;
         const uint8_t* src = blk_src(blk);
+        // any element size, staged: raw bytes into the table's LDS, bit
+        // transpose from there (before the table is zeroed)
+        bool staged = false;
+        if constexpr (EK == 0) {
+            if (raw_fits(m)) {
+                staged = true;
+                raw_to_lds(RW, L0, n, lane);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // lane = (group g, byte b) with b fastest: the 8 gathers of
+                // neighbouring lanes hit neighbouring bytes (no bank conflicts)
+                const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)E - 1) / (uint64_t)E);
+                for (int i = lane; i < P * E; i += kWave) {
+                    const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                    const lds8* x = L0 + 8 * g * E + b;
+                    uint64_t v = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) v |= (uint64_t)x[k * E] << (8 * k);
+                    v = tr8x8(v);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(v >> (8 * j));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
         // zero the hash table (LZ4_initStream) and the read pad behind the block
         for (int i = lane; i < kTableBytes / 16; i += kWave)
             ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
         if (lane < kDataPad / 4) ((lds32*)(D + ((n + 3) & ~3)))[lane] = 0;
         // bit transpose into LDS (bshuf_trans_bit_elem)
-        if constexpr (EK != 0) {
+        if (staged) {
+        } else if constexpr (EK != 0) {
             if (fits4(m)) {
                 transpose4_regs_to_lds<EK>(R4, D, P, lane);
             } else if (fits(m)) {
@@ -835,6 +893,11 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                     issue_block_loads4<EK>(R4, blk_src(next), mn / 8, lane);
                 else if (fits(mn))
                     issue_block_loads<EK>(R, blk_src(next), mn / 8, lane);
+            }
+        } else {
+            if (next < nb) {
+                const int mn = blk_m(next);
+                if (raw_fits(mn)) issue_raw_loads(RW, blk_src(next), mn * E, lane);
             }
         }
 
@@ -1150,7 +1213,8 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
         // table's LDS as staging (every block of up to ~16 KiB)
         const bool desc = !wide && 4 + lz4_bound((int)nmax) + 15 <= kTableBytes;
         const int32_t desc_off = (int32_t)(((nmax + 15) & ~15) + kDataPad);
-        EncArgs a{in, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off, nullptr, nullptr};
+        EncArgs a{in, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off, nullptr, nullptr,
+                  ((uintptr_t)in & 7) == 0 ? 1 : 0};
         const size_t lds = kTableBytes + (size_t)desc_off + (desc ? kDescBytes : 0);
         // the partial block decides its own table type, so a stream whose full
         // blocks need byU32 but partial block byU16 launches twice
@@ -1225,7 +1289,10 @@ hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
                 return hipErrorInvalidValue;  // mixed table types: the caller splits the batch
         const bool desc = !wide && 4 + lz4_bound((int)nmax) + 15 <= kTableBytes;
         const int32_t desc_off = (int32_t)(((nmax + 15) & ~15) + kDataPad);
-        EncArgs a{nullptr, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off, segs, blk_seg};
+        bool raw8 = true;
+        for (int i = 0; i < nsegs; i++) raw8 = raw8 && ((uintptr_t)hsegs[i].in & 7) == 0;
+        EncArgs a{nullptr, b.scratch, b.foot, b.slot, L, desc ? 1 : 0, desc_off, segs, blk_seg,
+                  raw8 ? 1 : 0};
         const size_t lds = kTableBytes + (size_t)desc_off + (desc ? kDescBytes : 0);
         bool aligned = true;
         for (int i = 0; i < nsegs; i++) aligned = aligned && ((uintptr_t)hsegs[i].in & 15) == 0;
