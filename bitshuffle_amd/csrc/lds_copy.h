@@ -56,8 +56,12 @@ __device__ __forceinline__ void lane_copy16(const lds8* S, int sp, lds8* Dd, int
 }
 
 // The whole wave copies n bytes whose source ends at or before the
-// destination starts (or lies in another buffer).  Long runs go as aligned
-// destination dwords built from two source dwords, edges byte-wise.
+// destination starts, lies in another buffer, or lies AFTER the destination
+// (sp > dp: a forward in-place copy, as the in-place decoder's literals).
+// Long runs go as aligned destination dwords built from two source dwords,
+// edges byte-wise.  The edge bytes are read before the dword loop and written
+// after it, and every 64-dword step reads before it writes, so no byte is
+// read after something else overwrote it.
 __device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int dp, int n, int lane) {
     if (n <= kWave) {
         if (lane < n) Dd[dp + lane] = S[sp + lane];
@@ -66,13 +70,15 @@ __device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int d
     const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
     const int head = q0 - dp, tailn = dp + n - q1;
     const int e = lane < 4 ? lane : n - tailn + (lane - 4);
-    if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn)) Dd[dp + e] = S[sp + e];
+    const bool edge = lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn);
+    const uint32_t eb = edge ? (uint32_t)S[sp + e] : 0u;
     const int nw = (q1 - q0) >> 2;
     for (int c = lane; c < nw; c += kWave) {
         const int s2 = sp + head + 4 * c;
         const lds32* w = (const lds32*)(S + (s2 & ~3));
         ((lds32*)(Dd + q0))[c] = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(s2 & 3));
     }
+    if (edge) Dd[dp + e] = (uint8_t)eb;
 }
 
 // Inclusive prefix sum over the 64 lanes with DPP moves (no LDS round trip):

@@ -399,7 +399,7 @@ __device__ __forceinline__ int read_ext(const Src& Cb, int& q, uint64_t w, int a
 // Phase 2 for one block.  The record payload starts at byte cp of the
 // 4-aligned LDS buffer Cb; pos[0..nseq) are its token positions (payload-
 // relative, validated by the scan); pos0 is this lane's prefetched pos[lane].
-template <class Src>
+template <bool kInPlace = false, class Src>
 __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8* D,
                                const uint32_t* __restrict__ pos, const int nseq, uint32_t pos0,
                                const int lane) {
@@ -437,11 +437,34 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
         const int op = opb + incl - len;
         opb += __builtin_amdgcn_readlane(incl, kWave - 1);
         // ---- literals: short runs per lane, long runs by the whole wave
-        if (lit > 0 && lit <= 16) Cb.copy16(lsrc, D, op, lit);
-        for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
-            const int l = ffs64(lm);
-            Cb.copyw(__builtin_amdgcn_readlane(lsrc, l), D, __builtin_amdgcn_readlane(op, l),
-                     __builtin_amdgcn_readlane(lit, l), lane);
+        if constexpr (!kInPlace) {
+            if (lit > 0 && lit <= 16) Cb.copy16(lsrc, D, op, lit);
+            for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
+                const int l = ffs64(lm);
+                Cb.copyw(__builtin_amdgcn_readlane(lsrc, l), D, __builtin_amdgcn_readlane(op, l),
+                         __builtin_amdgcn_readlane(lit, l), lane);
+            }
+        } else {
+            // the record sits in the output buffer: copies run in SEQUENCE
+            // order -- the short runs between two long ones as one parallel
+            // step (all of its reads precede its writes), each long run by the
+            // wave -- so no sequence's writes come before an earlier
+            // sequence's reads; the scan's margin test keeps every write below
+            // every later sequence's record bytes
+            const uint64_t sm = ballot(lit > 0 && lit <= 16);
+            uint64_t lm = ballot(lit > 16), done = 0;
+            for (;;) {
+                const int l = lm ? ffs64(lm) : kWave;
+                const uint64_t below = l >= kWave ? ~0ull : ((1ull << l) - 1ull);
+                if (sm & below & ~done) {
+                    if (((sm & below & ~done) >> lane) & 1ull) Cb.copy16(lsrc, D, op, lit);
+                }
+                if (l >= kWave) break;
+                done = below | (1ull << l);
+                Cb.copyw(__builtin_amdgcn_readlane(lsrc, l), D, __builtin_amdgcn_readlane(op, l),
+                         __builtin_amdgcn_readlane(lit, l), lane);
+                lm &= lm - 1;
+            }
         }
         // ---- matches, in batches of mutually independent sequences
         const int mop = op + lit;
@@ -479,6 +502,7 @@ struct DecArgs {
     const Seg* segs; // batch: per-stream table (nullptr: the single stream above)
     const uint32_t* blk_seg;
     int32_t stage_off;  // EK == 0: LDS offset of the output staging block (0: none)
+    int32_t ip_end;     // VAR & 512: the in-place record region ends at this LDS offset
 };
 
 // Where block k lives: its stream's framed bytes, output, token-position area
@@ -541,10 +565,17 @@ struct Span {
 // 16-byte chunks covering a record of an 8 KiB block: (8244 + 30) / 16 / 64 -> 9.
 constexpr int kPayIters = 9;
 
-struct PayRegs {
-    u32x4 v[kPayIters];
+// The in-place decoder prefetches only the first kPayItersIP granule rows
+// (5 KiB: every G1/G2 record of typical size) to stay within 96 VGPRs (5
+// waves per SIMD); a longer record's remainder is copied when it lands.
+constexpr int kPayItersIP = 5;
+
+template <int IT = kPayIters>
+struct PayRegsT {
+    u32x4 v[IT];
     uint32_t pos;  // token position of sequence `lane` (two-phase path)
 };
+using PayRegs = PayRegsT<>;
 
 // Record bytes [o0, o1) are read as whole 16-byte granules aligned on the
 // absolute address (a granule never crosses a page: the extra bytes at either
@@ -563,24 +594,32 @@ __device__ __forceinline__ bool span_fits(const DecArgs& a, const Span& sp) {
     return span_chunks(a, sp) <= kPayIters * kWave;
 }
 
-__device__ __forceinline__ void issue_pay(PayRegs& R, const DecArgs& a, const Span& sp, int lane) {
+template <int IT>
+__device__ __forceinline__ void issue_pay(PayRegsT<IT>& R, const DecArgs& a, const Span& sp, int lane) {
     const gbl128c* g4 = span_base(a, sp);
     const int nch = span_chunks(a, sp);
 #pragma unroll
-    for (int it = 0; it < kPayIters; it++) {
+    for (int it = 0; it < IT; it++) {
         const int c = it * kWave + lane;
         if (c < nch) R.v[it] = g4[c];
     }
     R.pos = sp.loc.seq[sp.o0 / 3 + lane];
 }
 
-__device__ __forceinline__ void land_pay(const PayRegs& R, const DecArgs& a, const Span& sp,
+// Lands the prefetched rows; rows beyond IT (a record longer than the
+// prefetch) come straight from global memory.
+template <int IT>
+__device__ __forceinline__ void land_pay(const PayRegsT<IT>& R, const DecArgs& a, const Span& sp,
                                          lds8* C, int lane) {
     const int nch = span_chunks(a, sp);
 #pragma unroll
-    for (int it = 0; it < kPayIters; it++) {
+    for (int it = 0; it < IT; it++) {
         const int c = it * kWave + lane;
         if (c < nch) ((lds128*)C)[c] = R.v[it];
+    }
+    if (IT * kWave < nch) {
+        const gbl128c* g4 = span_base(a, sp);
+        for (int c = IT * kWave + lane; c < nch; c += kWave) ((lds128*)C)[c] = g4[c];
     }
 }
 
@@ -673,15 +712,21 @@ struct GReader {
 // A quarter of the scattered position stores (each costs a whole write
 // transaction, and on gfx9's in-order vmcnt every store issued before a
 // window load is waited for with it).
+constexpr int kMxBias = 1 << 14;
+// Bytes behind the decoded block reserved for the in-place record (keeps one
+// buffer within 7 LDS granules = 8,960 bytes: 18 waves per CU)
+constexpr int kInPlaceMargin = 704;
 struct SeqOut {
     typedef __attribute__((address_space(1))) uint32_t g32;
     uint32_t* base;
     int ph;  // dword phase of base within its 16-byte chunk
     u32x4 buf;
+    int mx = -(1 << 20);  // max over sequences of (output start - token position)
     __device__ __forceinline__ static uint32_t sel(const u32x4 b, int s) {
         return s == 0 ? b.x : (s == 1 ? b.y : (s == 2 ? b.z : b.w));
     }
-    __device__ __forceinline__ void put(int i, uint32_t v) {
+    __device__ __forceinline__ void put(int i, uint32_t v, int op) {
+        mx = max(mx, op - (int)v);
         const int s = (ph + i) & 3;
         buf.x = s == 0 ? v : buf.x;
         buf.y = s == 1 ? v : buf.y;
@@ -733,6 +778,9 @@ __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
         const int r = scan_block(rd, (int)clen, n, out, cnt);
         out.flush(cnt);  // a rejected block's positions are never read
         st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
+        // valid: bits 32..47 carry max(output start - token position) + 2^14,
+        // the in-place decoder's safety margin test (kInPlace below)
+        if (st >= 0) st |= (int64_t)min(max(out.mx + kMxBias, 0), 0xFFFF) << 32;
     }
     a.status[k] = st;
 }
@@ -757,7 +805,8 @@ __device__ __forceinline__ void touch_done(const Touch& t) {
 }
 
 // Returns this lane's token position of the record (two-phase path).
-__device__ __forceinline__ uint32_t land_record(const PayRegs& R, bool in_regs, const DecArgs& a,
+template <int IT>
+__device__ __forceinline__ uint32_t land_record(const PayRegsT<IT>& R, bool in_regs, const DecArgs& a,
                                                 const Span& sp, lds8* Cbuf, int lane) {
     if (in_regs) {
         land_pay(R, a, sp, Cbuf, lane);
@@ -776,7 +825,8 @@ __device__ __forceinline__ uint32_t land_record(const PayRegs& R, bool in_regs, 
 // the completion of the previous block's stores (gfx9 counts loads and stores
 // on one in-order vmcnt) stalls the wave.
 template <int EK, int VAR>
-__global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 4 ? 4 : 5) : 1)))
+void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
     const int E = EK ? EK : a.L.E;
@@ -784,19 +834,32 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     lds8* Cbuf = to_lds(smem) + a.cap + 16;  // record bytes, 16-aligned base
     // VAR & 16: phase 2 reads the record from global memory (no LDS copy)
     constexpr bool kG = (VAR & 16) != 0;
+    // VAR & 512 (default): the record lands IN PLACE, at the end of the
+    // decoded block's own LDS buffer (LZ4 in-place decompression).  Sequence j
+    // writes output [op_j, ...) below its own token position, which the scan
+    // proved per block (bits 32..47 of its verdict: max(op_j - tp_j)); a
+    // block that fails the test reads its record from global memory instead.
+    // One ~8.9 KiB buffer per wave: every record read is an LDS read and the
+    // occupancy of the global-read decoder stays.
+    constexpr bool kIP = (VAR & 512) != 0;
+    auto cbuf_of = [&](const Span& sp) -> lds8* {
+        return kIP ? to_lds(smem) + a.ip_end - 16 * span_chunks(a, sp) : Cbuf;
+    };
     const int64_t stride = gridDim.x;
     int64_t blk = blockIdx.x;
     if (blk >= nb) return;
 
-    PayRegs R;
+    PayRegsT<kIP ? kPayItersIP : kPayIters> R;
+    // in place: every record is prefetched (partly, when long) into R
+    auto fits = [&](const Span& sp) { return kIP || span_fits(a, sp); };
     Span cur = span_from(a, issue_offs(a, blk, nb, lane), nb);
     uint32_t cur_pos;
     if constexpr (kG) {
         cur_pos = cur.loc.seq[cur.o0 / 3 + lane];
     } else {
-        const bool in_regs = span_fits(a, cur);
+        const bool in_regs = fits(cur);
         if (in_regs) issue_pay(R, a, cur, lane);
-        cur_pos = land_record(R, in_regs, a, cur, Cbuf, lane);
+        cur_pos = land_record(R, in_regs, a, cur, cbuf_of(cur), lane);
     }
     int64_t next = blk + stride;
     Span nxt = {};
@@ -810,7 +873,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
             pref_pos = nxt.loc.seq[nxt.o0 / 3 + lane];
             if constexpr (kTouch) t_nxt = touch_record(nxt, lane);
         } else {
-            nxt_in_regs = span_fits(a, nxt);
+            nxt_in_regs = fits(nxt);
             if (nxt_in_regs) issue_pay(R, a, nxt, lane);
         }
     }
@@ -822,7 +885,8 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
     for (;;) {
         const int P = cur.loc.m / 8;
         const int cp = span_shift(a, cur);
-        const lds8* C = Cbuf + cp;
+        lds8* const CB = cbuf_of(cur);
+        const lds8* C = CB + cp;
         // the scan's verdict: sequence count, or the block's error code
         int status = 0, clen = 0;
         if (cur.scan < 0) {
@@ -837,9 +901,18 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                 lz4_exec_block(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
         } else {
             clen = (int)(((uint32_t)C[0] << 24) | ((uint32_t)C[1] << 16) | ((uint32_t)C[2] << 8) | C[3]);
-            if (!(VAR & 64))
-                lz4_exec_block(LdsRec{Cbuf}, cp + 4, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan,
-                               cur_pos, lane);
+            const int mx = (int)((cur.scan >> 32) & 0xFFFF) - kMxBias;
+            if (!kIP || mx <= (int)(CB - D) + cp + 4) {
+                if (!(VAR & 64))
+                    lz4_exec_block<kIP>(LdsRec{CB}, cp + 4, D, cur.loc.seq + cur.o0 / 3,
+                                        (int)cur.scan, cur_pos, lane);
+            } else {
+                // too little room to decode in place: the record from L2
+                const uintptr_t b0 = (uintptr_t)(cur.loc.in + cur.o0 + 4);
+                const GblRec src{b0, (b0 + (uintptr_t)clen - 1) & ~(uintptr_t)3};
+                if (!(VAR & 64))
+                    lz4_exec_block(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -857,12 +930,12 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
                     pref_pos = nxt2.loc.seq[nxt2.o0 / 3 + lane];
                     if constexpr (kTouch) t_nxt2 = touch_record(nxt2, lane);
                 }
-            } else {
+            } else if constexpr (!kIP) {
                 nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
                 if (nn < nb) {
                     nxt2 = span_from(a, O, nb);
                     if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
-                    nxt2_in_regs = span_fits(a, nxt2);
+                    nxt2_in_regs = fits(nxt2);
                     if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
                 }
             }
@@ -936,6 +1009,21 @@ __global__ __launch_bounds__(64) void k_lz4_decode(DecArgs a, int64_t nb) {
             atomicMax(cur.loc.bad, (long long)blk);
         }
         if (lane == 0) a.status[blk] = status == 0 ? (int64_t)clen + 4 : (int64_t)status;
+        if constexpr (kIP) {
+            // the decoded block has left LDS: the next record lands in place,
+            // then the loads two ahead
+            if (next < nb) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                nxt_pos = land_record(R, nxt_in_regs, a, nxt, cbuf_of(nxt), lane);
+                if (nn < nb) {
+                    nxt2 = span_from(a, O, nb);
+                    if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                    nxt2_in_regs = fits(nxt2);
+                    if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
+                }
+            }
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         if (next >= nb) break;
@@ -1080,10 +1168,13 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     // phase 2 reads each record straight from global memory, so the LDS holds
     // only the decoded block: 18 resident waves per CU instead of 9 (A/B
     // variant 16: the record staged in LDS, as before)
-    const bool grec = tuning_variant() != 16;
+    const bool grec = tuning_variant() == 16 || tuning_variant() == 32;
     // ... and touches each record's lines two blocks ahead (variant 32: not)
-    const bool touch = grec && tuning_variant() != 32;
-    size_t lds = (size_t)a.cap + 16 + (grec ? 0 : rec);
+    const bool touch = tuning_variant() == 16;
+    // default: the record in place at the end of the block's own buffer
+    const bool inplace = !grec && tuning_variant() != 64;
+    a.ip_end = (int32_t)(((size_t)a.cap + kInPlaceMargin + 15) & ~(size_t)15);
+    size_t lds = inplace ? (size_t)a.ip_end + 32 : (size_t)a.cap + 16 + (grec ? 0 : rec);
     const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
     // any other element size: stage the inverse transpose in LDS when every
     // output is 8-aligned (a.stage_off was set to 1 by the caller as "may")
@@ -1096,9 +1187,9 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     const void* fn = nullptr;
 #define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
     switch (ek) {
-        case 1: fn = touch ? BSHUF_DEC(1, 48) : (grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0)); break;
+        case 1: fn = inplace ? BSHUF_DEC(1, 512) : touch ? BSHUF_DEC(1, 48) : (grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0)); break;
         case 2:
-            fn = touch ? BSHUF_DEC(2, 48) : (grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0));
+            fn = inplace ? BSHUF_DEC(2, 512) : touch ? BSHUF_DEC(2, 48) : (grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0));
 #ifdef BSHUF_DIAG
             // diagnostic build only -- ABLATIONS for timing, wrong output:
             // 8 no output stores, 64 no sequence execution
@@ -1108,15 +1199,15 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
 #endif
             break;
         case 4:
-            fn = touch ? BSHUF_DEC(4, 48) : (grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0));
+            fn = inplace ? BSHUF_DEC(4, 512) : touch ? BSHUF_DEC(4, 48) : (grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0));
 #ifdef BSHUF_DIAG
             if (diag_variant() == 8) fn = BSHUF_DEC(4, 56);
             if (diag_variant() == 64) fn = BSHUF_DEC(4, 112);
             if (diag_variant() == 72) fn = BSHUF_DEC(4, 120);
 #endif
             break;
-        case 8: fn = touch ? BSHUF_DEC(8, 48) : (grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0)); break;
-        default: fn = touch ? BSHUF_DEC(0, 48) : (grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0)); break;
+        case 8: fn = inplace ? BSHUF_DEC(8, 512) : touch ? BSHUF_DEC(8, 48) : (grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0)); break;
+        default: fn = inplace ? BSHUF_DEC(0, 512) : touch ? BSHUF_DEC(0, 48) : (grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0)); break;
     }
 #undef BSHUF_DEC
     hipError_t e = scan_impl(a, nb, s);

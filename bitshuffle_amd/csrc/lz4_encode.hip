@@ -335,6 +335,23 @@ struct CountOut {
     uint32_t tail;
 };
 
+// Equal bytes from the start of one 256-byte count window (va / vb: the a-
+// and b-side dword of every lane), capped at lim, the bytes the window may
+// count (mlimit - window start; <= 0: none).  256 means "all equal and the
+// limit lies beyond": count on.  The first differing lane comes straight
+// from the compare's ballot and its first differing byte from one readlane
+// (no per-lane byte counts, no second ballot).
+__device__ __forceinline__ int window_equal(uint32_t va, uint32_t vb, int lim) {
+    const uint64_t ne = ballot(va != vb);
+    int c = kWinBytes;
+    if (ne) {
+        const int f = ffs64(ne);
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)(va ^ vb), f);
+        c = 4 * f + (__builtin_ctz(x) >> 3);
+    }
+    return min(c, max(lim, 0));
+}
+
 // The re-test's match test and LZ4_count in one LDS round trip: counts the
 // equal bytes from ip itself (the first window's lane 0 is the 4-byte
 // test).  cnt = match length beyond kMinMatch, or -1 when there is no match.
@@ -342,30 +359,21 @@ __device__ __forceinline__ CountOut test_and_count(const lds8* D, int n, int ip,
                                                    int mlimit, int lane, uint32_t va0) {
     CountOut r;
     r.back = 0;
-    int pa = ip + 4 * lane, pb = ref + 4 * lane;
-    uint32_t va = va0, vb = lds_rd32(D, min(pb, n));  // va0: the a-side, read ahead
+    uint32_t va = va0, vb = lds_rd32(D, min(ref + 4 * lane, n));  // va0: the a-side, read ahead
     if (__builtin_amdgcn_readfirstlane(va ^ vb) != 0) {
         r.cnt = -1;
         return r;
     }
-    int total = 0;
-    for (;;) {
-        const uint32_t x = va ^ vb;
-        int eq = x ? (__ffs(x) - 1) >> 3 : 4;
-        eq = min(eq, max(mlimit - pa, 0));
-        const uint64_t full = ballot(eq == 4);
-        if (full != ~0ull) {
-            const int f = ffs64(~full);
-            r.cnt = total + 4 * f + __builtin_amdgcn_readlane(eq, f) - kMinMatch;
+    for (int total = 0;; total += kWinBytes) {
+        const int c = window_equal(va, vb, mlimit - (ip + total));
+        if (c < kWinBytes) {
+            r.cnt = total + c - kMinMatch;
             r.tail_base = ip + total;
             r.tail = va;
             return r;
         }
-        total += kWinBytes;
-        pa = ip + total + 4 * lane;
-        pb = ref + total + 4 * lane;
-        va = lds_rd32(D, min(pa, n));
-        vb = lds_rd32(D, min(pb, n));
+        va = lds_rd32(D, min(ip + total + kWinBytes + 4 * lane, n));
+        vb = lds_rd32(D, min(ref + total + kWinBytes + 4 * lane, n));
     }
 }
 
@@ -374,8 +382,7 @@ __device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip
     CountOut r;
     // first forward window and backward bytes together
     const int a = ip + kMinMatch, b = ref + kMinMatch;
-    int pa = a + 4 * lane, pb = b + 4 * lane;
-    uint32_t va = lds_rd32(D, min(pa, n)), vb = lds_rd32(D, min(pb, n));
+    uint32_t va = lds_rd32(D, min(a + 4 * lane, n)), vb = lds_rd32(D, min(b + 4 * lane, n));
     const int ba = ip - 1 - lane, bb = ref - 1 - lane;
     const uint32_t ca = D[max(ba, 0)], cb = D[max(bb, 0)];
     // backward
@@ -394,24 +401,16 @@ __device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip
         r.back = back;
     }
     // forward
-    int total = 0;
-    for (;;) {
-        const uint32_t x = va ^ vb;
-        int eq = x ? (__ffs(x) - 1) >> 3 : 4;
-        eq = min(eq, max(mlimit - pa, 0));
-        const uint64_t full = ballot(eq == 4);
-        if (full != ~0ull) {
-            const int f = ffs64(~full);
-            r.cnt = total + 4 * f + __builtin_amdgcn_readlane(eq, f);
+    for (int total = 0;; total += kWinBytes) {
+        const int c = window_equal(va, vb, mlimit - (a + total));
+        if (c < kWinBytes) {
+            r.cnt = total + c;
             r.tail_base = a + total;
             r.tail = va;
             return r;
         }
-        total += kWinBytes;
-        pa = a + total + 4 * lane;
-        pb = b + total + 4 * lane;
-        va = lds_rd32(D, min(pa, n));
-        vb = lds_rd32(D, min(pb, n));
+        va = lds_rd32(D, min(a + total + kWinBytes + 4 * lane, n));
+        vb = lds_rd32(D, min(b + total + kWinBytes + 4 * lane, n));
     }
 }
 

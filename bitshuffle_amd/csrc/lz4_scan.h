@@ -37,7 +37,8 @@ BSHUF_HD inline bool scan_len(Rd& rd, int& ip, int ilimit, bool initial_check, i
 // check different margins, so both are followed to reach the same accept /
 // reject decision and error position.  Records each sequence's token position.
 // Returns op (bytes the block decodes to) or -(ip)-1.  Token positions go to
-// out.put(i, pos) in increasing i (a rejected block may have put one more).
+// out.put(i, pos, op) in increasing i, with op the output position where that
+// sequence starts (a rejected block may have put one more).
 template <class Rd, class Out>
 BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, Out& out, int& cnt) {
     enum { kNone, kLit, kCopyMatch, kMatch };
@@ -58,7 +59,7 @@ BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, Out& out, in
                 entry = kLit;
             }
             if (entry == kNone) {
-                out.put(cnt++, (uint32_t)tp);
+                out.put(cnt++, (uint32_t)tp, op);
                 ip += len;
                 op += len;
                 off = (int)(rd(ip) | (rd(ip + 1) << 8));
@@ -86,7 +87,7 @@ BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, Out& out, in
             fast = false;  // the rest of the block runs in the safe loop
         } else {
             if (len != 15 && ip < clen - 16 && op <= n - 32) {
-                out.put(cnt++, (uint32_t)tp);
+                out.put(cnt++, (uint32_t)tp, op);
                 ip += len;
                 op += len;
                 ml = tok & 15;
@@ -106,7 +107,7 @@ BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, Out& out, in
             }
         }
         if (entry == kLit) {
-            out.put(cnt++, (uint32_t)tp);
+            out.put(cnt++, (uint32_t)tp, op);
             const int cpy = op + len;
             if (cpy > n - 12 || ip + len > clen - 8) {
                 // must be the last sequence: consume the input exactly

@@ -133,11 +133,11 @@ extern "C" {
 
 int bshuf_set_variant(int v) {
     // 2 inline LZ4 emitter, 4 one-group-per-lane transpose, 8 re-test table
-    // lookup by lane 0's returning exchange, 16 decoder stages each record in LDS, 32
-    // decoder without the two-blocks-ahead touch of each record's lines,
-    // 128 insert/readback
-    // search window (the fallback for devices without lane-ordered LDS atomics)
-    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 128) return -71;
+    // lookup by lane 0's returning exchange, decoder record access 16 global
+    // + touch / 32 global / 64 own LDS buffer (default: in place), 128
+    // insert/readback search window (the fallback for devices without
+    // lane-ordered LDS atomics)
+    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128) return -71;
     t_variant = v;
     return 0;
 }

@@ -11,7 +11,10 @@ struct HostReader {
 };
 struct HostOut {
     uint32_t* pos;
-    void put(int i, uint32_t v) { pos[i] = v; }
+    void put(int i, uint32_t v, int op) {
+        pos[i] = v;
+        (void)op;
+    }
 };
 }  // namespace
 

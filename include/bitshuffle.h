@@ -102,10 +102,11 @@ int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first,
 void bshuf_prof_enable(int on);
 /* Selects, for the CALLING THREAD only, an alternative kernel variant for A/B
  * measurements: 0 default, 2 inline LZ4 emitter, 4 one-group-per-lane
- * transpose, 8 re-test table lookup by lane 0's returning exchange, 16 decoder with each
- * record staged in LDS, 32 decoder without the record-line touch two blocks
- * ahead, 128 insert/read-back search window.  Every accepted variant
- * produces identical bytes; anything else is rejected with -71. */
+ * transpose, 8 re-test table lookup by lane 0's returning exchange, decoder
+ * record access 16 from global memory with a two-blocks-ahead touch / 32
+ * without it / 64 staged in an LDS buffer of its own (default: in place at the
+ * end of the block's LDS buffer), 128 insert/read-back search window.  Every
+ * accepted variant produces identical bytes; anything else is rejected with -71. */
 int bshuf_set_variant(int v);
 size_t bshuf_prof_collect(char* buf, size_t len);
 

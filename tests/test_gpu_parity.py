@@ -131,21 +131,22 @@ def _with_variant(bs, variant, fn):
 def test_variant_knob_rejects_ablations(bs):
     """Only byte-identical variants are accepted (and only for the calling
     thread); timing ablations are not in the product library."""
-    for v in (1, 48, 64, 68, 3, -1):
+    for v in (1, 48, 68, 3, -1, 512):
         assert bs.lib.bshuf_set_variant(v) == -71
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
     self-check fails), 2 the inline emitter (also the overflow path of the
     descriptor emitter), 4 the one-group-per-lane transpose, 8 the re-test
     table lookup by lane 0's returning exchange (the default: plain LDS ops by
-    every lane), 16 the decoder with each record staged in
-    LDS (the default reads records from global memory), 32 the decoder
-    without the two-blocks-ahead touch of each record's lines."""
+    every lane); decoder record access: 16 straight from global memory with
+    each record's lines touched two blocks ahead, 32 the same without the
+    touch, 64 staged in an LDS buffer of its own (the default decodes each
+    record in place at the end of its block's LDS buffer)."""
     rng = np.random.default_rng(128)
     cases = [oracle.gen_g1(3 * 4096 + 1005),
              (rng.integers(-2, 3, 50000).cumsum() % 97).astype(np.int16),
