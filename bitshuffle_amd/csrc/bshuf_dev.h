@@ -97,6 +97,9 @@ __device__ __forceinline__ lds8* to_lds(void* p) { return (lds8*)(p); }
 typedef __attribute__((address_space(1))) const u32x4 gbl128c;
 typedef __attribute__((address_space(1))) u32x4 gbl128;
 typedef __attribute__((address_space(1))) uint8_t gbl8;
+typedef __attribute__((address_space(1))) const u32x2 gbl64c;
+typedef __attribute__((address_space(1))) u32x2 gbl64;
+typedef __attribute__((address_space(1))) const uint8_t gbl8c;
 __device__ __forceinline__ const gbl128c* g128_aligned_down(const void* p) {
     return (const gbl128c*)((uintptr_t)p & ~(uintptr_t)15);
 }
@@ -209,13 +212,13 @@ __device__ __forceinline__ void untranspose4(const uint32_t (&pl)[8 * EK], uint3
 template <int EK>
 __device__ __forceinline__ void load_group(const uint8_t* p, uint32_t (&w)[2 * EK]) {
     if constexpr (EK == 1) {
-        const uint2 v = *reinterpret_cast<const uint2*>(p);
+        const u32x2 v = *(const gbl64c*)p;
         w[0] = v.x;
         w[1] = v.y;
     } else {
 #pragma unroll
         for (int i = 0; i < EK / 2; i++) {
-            const uint4 v = *reinterpret_cast<const uint4*>(p + 16 * i);
+            const u32x4 v = *(const gbl128c*)(p + 16 * i);
             w[4 * i + 0] = v.x;
             w[4 * i + 1] = v.y;
             w[4 * i + 2] = v.z;
@@ -224,6 +227,7 @@ __device__ __forceinline__ void load_group(const uint8_t* p, uint32_t (&w)[2 * E
     }
 }
 
+// The 8*EK bytes of one group, from 2*EK words.
 template <int EK>
 __device__ __forceinline__ void store_group(uint8_t* p, const uint32_t (&w)[2 * EK]) {
     if constexpr (EK == 1) {

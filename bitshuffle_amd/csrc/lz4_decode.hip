@@ -336,7 +336,6 @@ struct LdsRec {
 };
 
 typedef __attribute__((address_space(1))) const uint32_t gbl32c;
-typedef __attribute__((address_space(1))) const uint8_t gbl8c;
 
 struct GblRec {
     uintptr_t base;   // absolute address of payload byte 0
@@ -940,12 +939,18 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
                 }
             }
         }
-        if (status == 0 && !(VAR & 8)) {
+        if (status != 0) {
+            if (lane == 0) atomicMax(cur.loc.bad, (long long)blk);
+        } else if (!(VAR & 8)) {
             uint8_t* dst = cur.loc.out;
             if constexpr (EK != 0) {
                 // four groups per lane (EK <= 4; 8-byte elements would hold
                 // 192 registers): one LDS dword per plane, the bit-sliced
-                // transpose of untranspose4, 32*EK contiguous bytes out
+                // transpose of untranspose4, 32*EK contiguous bytes out.
+                // (Reordering the groups through LDS for fully coalesced
+                // stores sped the store path up -- 0.94 -> 0.60 ms without
+                // sequence execution, 2 GiB G1 -- but slowed the whole kernel
+                // 2-8 %: the decode is issue-bound, not store-bound.)
                 const int P4 = (EK <= 4 && (P & 3) == 0) ? P >> 2 : 0;
                 const lds32* D32 = (const lds32*)D;
                 for (int q = lane; q < P4; q += kWave) {
@@ -990,8 +995,7 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
                 __builtin_amdgcn_wave_barrier();
                 const int nw = P * E;  // 8-byte words of the block
                 for (int i = lane; i < nw; i += kWave) {
-                    const u32x2 v = ((const lds64v*)S)[i];
-                    reinterpret_cast<uint2*>(dst)[i] = make_uint2(v.x, v.y);
+                    ((gbl64*)dst)[i] = ((const lds64v*)S)[i];
                 }
             } else {
                 for (int i = lane; i < P * E; i += kWave) {
@@ -1002,11 +1006,9 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
                     v = tr8x8(v);
 #pragma unroll
                     for (int k = 0; k < 8; k++)
-                        dst[(int64_t)(8 * g + k) * E + b] = (uint8_t)(v >> (8 * k));
+                        ((gbl8*)dst)[(int64_t)(8 * g + k) * E + b] = (uint8_t)(v >> (8 * k));
                 }
             }
-        } else if (lane == 0) {
-            atomicMax(cur.loc.bad, (long long)blk);
         }
         if (lane == 0) a.status[blk] = status == 0 ? (int64_t)clen + 4 : (int64_t)status;
         if constexpr (kIP) {
@@ -1193,17 +1195,17 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
 #ifdef BSHUF_DIAG
             // diagnostic build only -- ABLATIONS for timing, wrong output:
             // 8 no output stores, 64 no sequence execution
-            if (diag_variant() == 8) fn = BSHUF_DEC(2, 56);
-            if (diag_variant() == 64) fn = BSHUF_DEC(2, 112);
-            if (diag_variant() == 72) fn = BSHUF_DEC(2, 120);
+            if (diag_variant() == 8) fn = BSHUF_DEC(2, 520);
+            if (diag_variant() == 64) fn = BSHUF_DEC(2, 576);
+            if (diag_variant() == 72) fn = BSHUF_DEC(2, 584);
 #endif
             break;
         case 4:
             fn = inplace ? BSHUF_DEC(4, 512) : touch ? BSHUF_DEC(4, 48) : (grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0));
 #ifdef BSHUF_DIAG
-            if (diag_variant() == 8) fn = BSHUF_DEC(4, 56);
-            if (diag_variant() == 64) fn = BSHUF_DEC(4, 112);
-            if (diag_variant() == 72) fn = BSHUF_DEC(4, 120);
+            if (diag_variant() == 8) fn = BSHUF_DEC(4, 520);
+            if (diag_variant() == 64) fn = BSHUF_DEC(4, 576);
+            if (diag_variant() == 72) fn = BSHUF_DEC(4, 584);
 #endif
             break;
         case 8: fn = inplace ? BSHUF_DEC(8, 512) : touch ? BSHUF_DEC(8, 48) : (grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0)); break;

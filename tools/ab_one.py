@@ -34,5 +34,5 @@ torch.cuda.synchronize()
 k = bench.prof_collect(B.lib)
 out = {name: round(ms / cnt, 4) for name, (cnt, ms) in k.items() if ms / cnt > 0.02}
 out["sha"] = h
-out["lib"] = os.path.basename(os.path.dirname(os.environ.get("BSHUF_LIB", "default/x")))
+out["lib"] = os.path.basename(os.environ.get("BSHUF_LIB", "default"))
 print(json.dumps(out), flush=True)
