@@ -1,7 +1,12 @@
 """HBM traffic per launch from rocprofv3 --pmc passes (tools/pmc.sh with
-tools/pmc_traffic_sets.txt), corrected as /opt/skills/guides/MI355X_MICROARCH.md
-prescribes for gfx950: FETCH_SIZE (KB) reads exactly 1/2 of a wide coalesced
-streaming read, so it is doubled; WRITE_SIZE (KB) is taken as is.
+tools/pmc_traffic_sets.txt).  FETCH_SIZE (KB) is corrected per access shape
+with the factors measured by tools/fetch_probe.hip on gfx950
+(profiles/r03/fetch_probe/calibration.json): coalesced 4/8/16-byte-per-lane
+loads and 16-byte loads of unaligned records all read 1/2 of their bytes
+(x2, the guide's rule); k_seq_scan's lane-divergent 32-byte window loads
+read 1/1.63 (x1.63).  WRITE_SIZE (KB) is taken as is (exact for coalesced and
+64-byte-per-lane stores; lane-divergent 16-byte stores, k_seq_scan's token
+positions, count ~3.4x their bytes).
 Writes profiles/pmc_traffic.json: {kernel: bytes per launch}, which bench.py
 reports as roofline.traffic for the dominant kernel.
 Usage: python tools/pmc_traffic.py gpurun_out/<tag> [out.json]"""
@@ -23,14 +28,18 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         if not m:
             continue
         vals[m.group(1)][r["Counter_Name"]].append(float(r["Counter_Value"]))
-res = {"_method": "per launch: 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 bytes (gfx950 FETCH_SIZE "
-                  "halving corrected); from rocprofv3 --pmc passes over tools/run_codec_once.py",
+# FETCH_SIZE correction per kernel (access shape), from the probe calibration
+FETCH_CORR = {"k_seq_scan": 1.6295}
+res = {"_method": "per launch: c*FETCH_SIZE*1024 + WRITE_SIZE*1024 bytes, c = 2 for coalesced "
+                  "and record loads, 1.63 for k_seq_scan's lane-divergent 32-B windows (measured: "
+                  "profiles/r03/fetch_probe/calibration.json); from rocprofv3 --pmc passes over "
+                  "tools/run_codec_once.py",
        "_source": d}
 for k, c in vals.items():
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         f = sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
         w = sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
-        res[k] = round(2 * f * 1024 + w * 1024)
+        res[k] = round(FETCH_CORR.get(k, 2.0) * f * 1024 + w * 1024)
         res[k + "_raw_KB"] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
