@@ -100,6 +100,7 @@ typedef __attribute__((address_space(1))) uint8_t gbl8;
 typedef __attribute__((address_space(1))) const u32x2 gbl64c;
 typedef __attribute__((address_space(1))) u32x2 gbl64;
 typedef __attribute__((address_space(1))) const uint8_t gbl8c;
+typedef __attribute__((address_space(1))) const uint32_t gbl32c;
 __device__ __forceinline__ const gbl128c* g128_aligned_down(const void* p) {
     return (const gbl128c*)((uintptr_t)p & ~(uintptr_t)15);
 }

@@ -100,6 +100,9 @@ int64_t max_device_block_bytes();
 int64_t max_lds_encode_bytes();
 int64_t max_lds_decode_bytes();
 constexpr int64_t kLargeTableWords = 8192;
+// wave-parallel parse of blocks above max_lds_encode_bytes (lz4_encode.hip):
+// shuf holds the bit-transposed blocks (64 bytes of pad behind the last)
+hipError_t launch_encode_big(const uint8_t* shuf, const Layout& L, const EncodeBufs& b, hipStream_t s);
 hipError_t launch_encode_large(const uint8_t* in, const Layout& L, const EncodeBufs& b,
                                uint8_t* shuf, uint32_t* tables, hipStream_t s);
 
@@ -127,6 +130,9 @@ hipError_t launch_index(const uint8_t* in, int64_t blocks_end, const Layout& L,
 hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
                          hipStream_t s);
+// wave-parallel execution of blocks above max_lds_decode_bytes (lz4_decode.hip)
+hipError_t launch_exec_big(const uint8_t* in, const Layout& L, const DecodeBufs& b, uint8_t* shuf,
+                           hipStream_t s);
 hipError_t launch_decode_large(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                                const DecodeBufs& b, uint8_t* shuf, hipStream_t s);
 // Batch versions: L.nfull = total blocks; b.idx_err and b.bad hold one word

@@ -157,8 +157,23 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
             }
         }
     } else {
-        for (int64_t c = cs + lane; c < cend; c += kWave)
-            if (c + 4 <= Cb) try_cand(c, be32_global(in + c));
+        // window larger than the LDS budget (large blocks): the same 4
+        // candidates per lane from three absolute-aligned global dwords (an
+        // aligned dword never crosses a page; bytes past Cb are never used),
+        // several iterations' loads in flight at once
+#pragma unroll 8
+        for (int64_t c0 = cs + 4 * lane; c0 < cend; c0 += 4 * kWave) {
+            const uintptr_t ap = (uintptr_t)(in + c0), al = ap & ~(uintptr_t)3;
+            const uint32_t sh = (uint32_t)(ap & 3);
+            const uint32_t w0 = *(const gbl32c*)al, w1 = *(const gbl32c*)(al + 4),
+                           w2 = *(const gbl32c*)(al + 8);
+            const uint32_t a = __builtin_amdgcn_alignbyte(w1, w0, sh), b = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t le = __builtin_amdgcn_alignbyte(b, a, (uint32_t)k);
+                try_cand(c0 + k, __builtin_bswap32(le));
+            }
+        }
     }
     for (int o = 32; o >= 1; o >>= 1) {
         lo = min(lo, (int64_t)__shfl_xor(lo, o));
@@ -335,7 +350,6 @@ struct LdsRec {
     }
 };
 
-typedef __attribute__((address_space(1))) const uint32_t gbl32c;
 
 struct GblRec {
     uintptr_t base;   // absolute address of payload byte 0
@@ -784,6 +798,69 @@ __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     a.status[k] = st;
 }
 
+// Blocks above max_lds_decode_bytes: one WAVE per block runs the same scan
+// (a lane-per-block walk of a ~100 KiB record pays a global round trip every
+// 32 bytes).  All 64 lanes step the state machine in lockstep on the same
+// bytes -- so the control flow stays uniform -- and the record streams
+// through an LDS window, refilled 8 KiB at a time by the whole wave with
+// coalesced 16-byte loads; only lane 0 stores the token positions.
+constexpr int kScanWin = 8192;
+struct WaveReader {
+    const uint8_t* P;
+    int clen;
+    int w0;  // record position of window byte 0
+    lds8* W;
+    int lane;
+    __device__ __forceinline__ uint32_t operator()(int p) {
+        if ((unsigned)(p - w0) >= (unsigned)kScanWin) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uintptr_t ap = (uintptr_t)(P + p);
+            w0 = p - (int)(ap & 15);
+            const gbl128c* q = g128_aligned_down(P + p);
+            for (int c = lane; c < kScanWin / 16; c += kWave)
+                if (w0 + 16 * c < clen) ((lds128*)W)[c] = q[c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        return W[p - w0];
+    }
+};
+struct SeqOutLane0 {
+    SeqOut o;
+    int lane;
+    __device__ __forceinline__ void put(int i, uint32_t v, int op) {
+        if (lane == 0) o.put(i, v, op);
+    }
+};
+
+__global__ __launch_bounds__(64) void k_seq_scan_big(DecArgs a, int64_t nb) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kScanWin];
+    const int lane = threadIdx.x;
+    const int64_t k = blockIdx.x;
+    const BlockLoc loc = block_loc(a, k, nb, a.segs ? a.blk_seg[k] : 0u);
+    const int n = loc.m * a.L.E;
+    int64_t o0 = (int64_t)a.offs[k];
+    int64_t o1 = !loc.last ? (int64_t)a.offs[k + 1] : o0 + 4 + (int64_t)a.maxlen;
+    clamp_span(o0, o1, loc.in_nbytes, a.maxlen);
+    const int64_t avail = o1 - o0;
+    const int64_t clen = avail >= 4 ? (int64_t)(int32_t)be32_global(loc.in + o0) : 0;
+    int64_t st = header_status(clen, avail, loc.last, a.maxlen);
+    if (st == 0) {
+        int cnt = 0;
+        WaveReader rd{loc.in + o0 + 4, (int)clen, -(1 << 30), to_lds(win), lane};
+        SeqOutLane0 out;
+        out.lane = lane;
+        out.o.base = loc.seq + o0 / 3;
+        out.o.ph = (int)(((uintptr_t)out.o.base >> 2) & 3);
+        out.o.buf = u32x4{0u, 0u, 0u, 0u};
+        const int r = scan_block(rd, (int)clen, n, out, cnt);
+        if (lane == 0) out.o.flush(cnt);
+        st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
+    }
+    if (lane == 0) a.status[k] = st;
+}
+
 // VAR & 32: one dword of every 128-byte line of a record, loaded two blocks
 // ahead so that phase 2's reads of it hit L2; the values are never used.
 struct Touch {
@@ -1067,7 +1144,125 @@ __global__ __launch_bounds__(256) void k_decode_finish(const int64_t* __restrict
     }
 }
 
+// Blocks above max_lds_decode_bytes: one wave per block executes the
+// sequences k_seq_scan validated (token positions in seq, verdict in status)
+// into the block's slice of the global scratch, the same way lz4_exec_block
+// does in LDS: 64 sequences decoded at once, a prefix sum places them, all
+// literal runs copied in parallel, the matches in batches of sequences that
+// cannot depend on each other.  The output is global memory, so a
+// workgroup-scope fence (the stores complete; the CU's L1 is write-through)
+// separates every batch from the next one that may read it.
+__device__ __forceinline__ void gbl_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
+
+// the whole wave runs one match D[mop, mop+ml) from mop-off (LZ4 semantics;
+// offset 0 writes zeros, lz4/lz4.c:501, 2407)
+__device__ __forceinline__ void gbl_match(gbl8* D, int mop, int off, int ml, int lane) {
+    if (off == 0) {
+        for (int i = lane; i < ml; i += kWave) D[mop + i] = 0;
+    } else if (off >= ml) {
+        for (int i = lane; i < ml; i += kWave) D[mop + i] = D[mop - off + i];
+    } else {
+        const float rinv = 1.0f / (float)off;
+        for (int i = lane; i < ml; i += kWave) D[mop + i] = D[mop - off + small_mod(i, off, rinv)];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_lz4_exec_big(const uint8_t* __restrict__ in,
+                                                      const uint64_t* __restrict__ offs,
+                                                      int64_t* __restrict__ status,
+                                                      const uint32_t* __restrict__ seq, Layout L,
+                                                      uint8_t* __restrict__ shuf, long long* bad) {
+    const int lane = threadIdx.x;
+    const int64_t k = blockIdx.x;
+    const int64_t st = status[k];
+    if (st < 0) {
+        if (lane == 0) atomicMax(bad, (long long)k);
+        return;
+    }
+    const int64_t o0 = (int64_t)offs[k];
+    const uint8_t* rec = in + o0;
+    const int clen = (int)be32_global(rec);
+    const uintptr_t b0 = (uintptr_t)(rec + 4);
+    const GblRec Cb{b0, (b0 + (uintptr_t)clen - 1) & ~(uintptr_t)3};
+    const gbl8c* P = (const gbl8c*)b0;
+    gbl8* D = (gbl8*)(shuf + k * (int64_t)L.bs * L.E);
+    const uint32_t* pos = seq + o0 / 3;
+    const int nseq = (int)st;
+    int opb = 0;
+    for (int c0 = 0; c0 < nseq; c0 += kWave) {
+        const int j = c0 + lane;
+        const bool act = j < nseq;
+        const int p = act ? (int)pos[j] : 0;
+        // ---- sequence fields, lane = sequence (as lz4_exec_block)
+        const uint64_t x = Cb.rd64(p);
+        const int tok = (int)(x & 255u);
+        int lit = act ? tok >> 4 : 0;
+        int q = p + 1;
+        if (lit == 15) lit += read_ext(Cb, q, x >> 8, 7);
+        const int lsrc = q;
+        q += lit;
+        int off = 0, ml = 0;
+        if (act && j + 1 < nseq) {
+            const int d = q - p;
+            const uint64_t y = d <= 6 ? x >> (8 * d) : Cb.rd64(q);
+            const int yav = d <= 6 ? 8 - d : 8;
+            off = (int)(y & 0xFFFFu);
+            q += 2;
+            ml = tok & 15;
+            if (ml == 15) ml += read_ext(Cb, q, y >> 16, yav - 2);
+            ml += kMinMatch;
+        }
+        const int len = lit + ml;
+        const int incl = wave_incl_sum(len, lane);
+        const int op = opb + incl - len;
+        opb += __builtin_amdgcn_readlane(incl, kWave - 1);
+        // ---- literals (record -> disjoint output ranges): short runs per
+        // lane, long runs by the whole wave
+        if (lit > 0 && lit <= 16)
+            for (int i = 0; i < lit; i++) D[op + i] = P[lsrc + i];
+        for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
+            const int l = ffs64(lm);
+            const int o = __builtin_amdgcn_readlane(op, l), sp = __builtin_amdgcn_readlane(lsrc, l);
+            const int nl = __builtin_amdgcn_readlane(lit, l);
+            for (int i = lane; i < nl; i += kWave) D[o + i] = P[sp + i];
+        }
+        gbl_fence();
+        // ---- matches, in batches of mutually independent sequences
+        const int mop = op + lit;
+        uint64_t todo = ballot(ml > 0);
+        while (todo) {
+            const int f = ffs64(todo);
+            const int opf = __builtin_amdgcn_readlane(mop, f);
+            const bool stop = lane > f && ml > 0 && (off < ml || mop - off + ml > opf);
+            const uint64_t sm = ballot(stop);
+            const int g = sm ? ffs64(sm) : kWave;
+            const bool inb = lane >= f && lane < g && ml > 0;
+            const bool coop = inb && (ml > 16 || off < ml);
+            if (inb && !coop)
+                for (int i = 0; i < ml; i++) D[mop + i] = D[mop - off + i];
+            for (uint64_t cm = ballot(coop); cm; cm &= cm - 1) {
+                const int l = ffs64(cm);
+                gbl_match(D, __builtin_amdgcn_readlane(mop, l), __builtin_amdgcn_readlane(off, l),
+                          __builtin_amdgcn_readlane(ml, l), lane);
+            }
+            gbl_fence();
+            todo &= g >= kWave ? 0ull : (~0ull << g);
+        }
+    }
+    if (lane == 0) status[k] = (int64_t)clen + 4;
+}
+
 }  // namespace
+
+hipError_t launch_exec_big(const uint8_t* in, const Layout& L, const DecodeBufs& b, uint8_t* shuf,
+                           hipStream_t s) {
+    const int64_t nb = L.nblocks();
+    if (nb == 0) return hipSuccess;
+    ProfScope prof("k_lz4_exec_big", s);
+    hipLaunchKernelGGL(k_lz4_exec_big, dim3((unsigned)nb), dim3(kWave), 0, s, in, b.offs, b.status, b.seq,
+                       L, shuf, b.bad);
+    return hipGetLastError();
+}
 
 int64_t index_chunk_bytes(const Layout& L) {
     const int64_t foot = 4 + lz4_bound(L.bs * L.E);
@@ -1155,6 +1350,12 @@ hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_
 }
 
 namespace {
+
+hipError_t scan_big_impl(DecArgs& a, int64_t nb, hipStream_t s) {
+    ProfScope prof("k_seq_scan_big", s);
+    hipLaunchKernelGGL(k_seq_scan_big, dim3((unsigned)nb), dim3(kWave), 0, s, a, nb);
+    return hipGetLastError();
+}
 
 hipError_t scan_impl(DecArgs& a, int64_t nb, hipStream_t s) {
     ProfScope prof("k_seq_scan", s);
@@ -1266,8 +1467,9 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
                   (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr,
                   ((uintptr_t)out & 7) == 0 ? 1 : 0};
         if (nmax > max_lds_decode_bytes()) {
-            // large blocks: validated by the same scan, executed in global memory
-            e = scan_impl(a, nb, s);
+            // large blocks: validated by the same scan (a wave per block),
+            // executed in global memory
+            e = tuning_variant() == 1024 ? scan_impl(a, nb, s) : scan_big_impl(a, nb, s);
             if (e == hipSuccess) e = launch_decode_large(in, in_nbytes, out, L, b, b.shuf, s);
         } else {
             e = decode_impl(a, nb, ((uintptr_t)out & 15) == 0, s);

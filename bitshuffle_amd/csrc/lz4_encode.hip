@@ -171,8 +171,33 @@ struct Table {
     }
 };
 
-template <bool WIDE>
-__device__ __forceinline__ uint32_t hash_at(const lds8* D, int p) {
+// A block in GLOBAL memory (blocks too large for the LDS, k_lz4_encode_big):
+// the same reads as the LDS block's, from aligned dwords of the transposed
+// scratch (which is padded, so reads up to 12 bytes past a block stay inside
+// it; those bytes never decide anything, as with the LDS block's pad).
+struct GblBlk {
+    const uint8_t* p;
+    __device__ __forceinline__ uint32_t operator[](int i) const { return ((const gbl8c*)p)[i]; }
+    __device__ __forceinline__ uint32_t w32(int a) const { return *(const gbl32c*)(p + a); }
+};
+// (the LDS overloads live in bshuf_dev.h, outside this unnamed namespace)
+using bshuf::lds_rd32;
+using bshuf::lds_rd64;
+__device__ __forceinline__ uint32_t lds_rd32(const GblBlk& D, int p) {
+    const int a = p & ~3;
+    return __builtin_amdgcn_alignbyte(D.w32(a + 4), D.w32(a), (uint32_t)(p & 3));
+}
+__device__ __forceinline__ uint64_t lds_rd64(const GblBlk& D, int p) {
+    const int a = p & ~3;
+    const uint32_t s = (uint32_t)(p & 3), w0 = D.w32(a), w1 = D.w32(a + 4), w2 = D.w32(a + 8);
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, s) |
+           ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32);
+}
+__device__ __forceinline__ uint32_t blk_w32(const lds8* D, int a) { return *(const lds32*)(D + a); }
+__device__ __forceinline__ uint32_t blk_w32(const GblBlk& D, int a) { return D.w32(a); }
+
+template <bool WIDE, class Blk>
+__device__ __forceinline__ uint32_t hash_at(const Blk& D, int p) {
     if constexpr (WIDE)
         return hash5(lds_rd64(D, p));
     else
@@ -222,23 +247,24 @@ struct EmitDesc {
     }
 };
 
+template <class Blk = const lds8*>
 struct EmitBytes {
     uint8_t* out;
-    const lds8* D_;  // the block (literal source)
+    Blk D_;  // the block (literal source)
     int lane;
     __device__ __forceinline__ void byte(int& op, uint32_t b) {
-        if (lane == 0) out[op] = (uint8_t)b;
+        if (lane == 0) ((gbl8*)out)[op] = (uint8_t)b;
         op++;
     }
     __device__ __forceinline__ void len(int& op, int v) {
         const int nb = v / 255 + 1;
         const uint8_t last = (uint8_t)(v - 255 * (nb - 1));
-        for (int i = lane; i < nb; i += kWave) out[op + i] = (i < nb - 1) ? (uint8_t)255 : last;
+        for (int i = lane; i < nb; i += kWave) ((gbl8*)out)[op + i] = (i < nb - 1) ? (uint8_t)255 : last;
         op += nb;
     }
-    __device__ __forceinline__ void copy(int& op, const lds8* D, int from, int n) {
+    __device__ __forceinline__ void copy(int& op, const Blk& D, int from, int n) {
         if (n <= kWave) {
-            if (lane < n) out[op + lane] = D[from + lane];
+            if (lane < n) ((gbl8*)out)[op + lane] = (uint8_t)D[from + lane];
         } else {
             // long runs (the last literals above all): 16-byte stores to the
             // ABSOLUTE 16-byte chunks inside the run, composed from five LDS
@@ -247,13 +273,14 @@ struct EmitBytes {
             const uintptr_t q0 = (a0 + 15) & ~(uintptr_t)15, q1 = a1 & ~(uintptr_t)15;
             const int head = (int)(q0 - a0), tailn = (int)(a1 - q1);
             const int e = lane < 16 ? lane : n - tailn + (lane - 16);
-            if (lane < 16 ? lane < head : lane - 16 < tailn) out[op + e] = D[from + e];
+            if (lane < 16 ? lane < head : lane - 16 < tailn) ((gbl8*)out)[op + e] = (uint8_t)D[from + e];
             const int nch = (int)((q1 - q0) >> 4);
             for (int c = lane; c < nch; c += kWave) {
                 const int s = from + head + 16 * c;
-                const lds32* w = (const lds32*)(D + (s & ~3));
+                const int a = s & ~3;
                 const uint32_t sh = (uint32_t)(s & 3);
-                const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+                const uint32_t x0 = blk_w32(D, a), x1 = blk_w32(D, a + 4), x2 = blk_w32(D, a + 8),
+                               x3 = blk_w32(D, a + 12), x4 = blk_w32(D, a + 16);
                 *(gbl128*)(q0 + 16 * (uintptr_t)c) =
                     u32x4{__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
                           __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
@@ -355,7 +382,8 @@ __device__ __forceinline__ int window_equal(uint32_t va, uint32_t vb, int lim) {
 // The re-test's match test and LZ4_count in one LDS round trip: counts the
 // equal bytes from ip itself (the first window's lane 0 is the 4-byte
 // test).  cnt = match length beyond kMinMatch, or -1 when there is no match.
-__device__ __forceinline__ CountOut test_and_count(const lds8* D, int n, int ip, int ref,
+template <class Blk>
+__device__ __forceinline__ CountOut test_and_count(const Blk& D, int n, int ip, int ref,
                                                    int mlimit, int lane, uint32_t va0) {
     CountOut r;
     r.back = 0;
@@ -377,14 +405,15 @@ __device__ __forceinline__ CountOut test_and_count(const lds8* D, int n, int ip,
     }
 }
 
-__device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip, int ref,
+template <class Blk>
+__device__ __forceinline__ CountOut catch_and_count(const Blk& D, int n, int ip, int ref,
                                                     int anchor, int mlimit, int lane) {
     CountOut r;
     // first forward window and backward bytes together
     const int a = ip + kMinMatch, b = ref + kMinMatch;
     uint32_t va = lds_rd32(D, min(a + 4 * lane, n)), vb = lds_rd32(D, min(b + 4 * lane, n));
     const int ba = ip - 1 - lane, bb = ref - 1 - lane;
-    const uint32_t ca = D[max(ba, 0)], cb = D[max(bb, 0)];
+    const uint32_t ca = (uint32_t)D[max(ba, 0)], cb = (uint32_t)D[max(bb, 0)];
     // backward
     {
         uint64_t cm = ballot(ba >= anchor && bb >= 0 && ca == cb);
@@ -392,7 +421,7 @@ __device__ __forceinline__ CountOut catch_and_count(const lds8* D, int n, int ip
         if (back == kWave) {
             for (int base = kWave;; base += kWave) {
                 const int xa = ip - 1 - base - lane, xb = ref - 1 - base - lane;
-                cm = ballot(xa >= anchor && xb >= 0 && D[max(xa, 0)] == D[max(xb, 0)]);
+                cm = ballot(xa >= anchor && xb >= 0 && (uint32_t)D[max(xa, 0)] == (uint32_t)D[max(xb, 0)]);
                 const int run = (~cm) ? ffs64(~cm) : kWave;
                 back = base + run;
                 if (run < kWave) break;
@@ -445,8 +474,8 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
 // Returns the compressed size, or -1 when the emitter ran out of descriptor
 // slots.  Mirrors lz4/lz4.c:1002-1331 for noDict, acceleration 1, notLimited
 // output.
-template <bool WIDE, bool READBACK, int OPT, class Emit>
-__device__ int lz4_encode_block(const lds8* D, const int n, const Table<WIDE> T, Emit& em,
+template <bool WIDE, bool READBACK, int OPT, class Emit, class Blk>
+__device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, Emit& em,
                                 const int lane) {
     DIAG_DECL
     int op = 0, anchor = 0;
@@ -934,7 +963,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
             }
         }
         if (c < 0) {
-            EmitBytes em{out + 4, D, lane};
+            EmitBytes<> em{out + 4, D, lane};
             c = lz4_encode_block<WIDE, kReadback, (VAR & 8)>(D, n, T, em, lane);
             if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         }
@@ -1039,6 +1068,36 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
     }
 }
 
+// Blocks too large for the LDS (above max_lds_encode_bytes): one wave per
+// block runs the same wave-parallel parse (lz4_encode_block) with only the
+// 16 KiB hash table in LDS -- byU32/hash5 from 65547 bytes, as
+// LZ4_compress_default picks (lz4/lz4.c:1388-1393) -- and the bit-transposed
+// block read from the global scratch (GblBlk); the LZ4 bytes go straight to
+// the block's scratch slot (EmitBytes).  16 KiB of LDS per wave: up to 10
+// blocks resident per CU.
+template <bool READBACK>
+__global__ __launch_bounds__(64) void k_lz4_encode_big(const uint8_t* __restrict__ shuf, Layout L,
+                                                       uint8_t* __restrict__ scratch, int64_t slot,
+                                                       uint64_t* __restrict__ foot) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x;
+    const int64_t k = blockIdx.x;
+    const int m = k < L.nfull ? L.bs : L.last;
+    const int n = m * L.E;
+    lds8* const tb = to_lds(smem);
+    for (int i = lane; i < kTableBytes / 16; i += kWave) ((lds128*)tb)[i] = u32x4{0u, 0u, 0u, 0u};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint8_t* out = scratch + k * slot;
+    const GblBlk D{shuf + k * (int64_t)L.bs * L.E};
+    EmitBytes<GblBlk> em{out + 4, D, lane};
+    // a short last block below 65547 bytes takes the byU16 table, as LZ4 does
+    const int c = n >= kU16TableLimit ? lz4_encode_block<true, READBACK, 0>(D, n, Table<true>{tb}, em, lane)
+                                      : lz4_encode_block<false, READBACK, 0>(D, n, Table<false>{tb}, em, lane);
+    if (lane < 4) ((gbl8*)out)[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
+    if (lane == 0) foot[k] = 4 + (uint64_t)c;
+}
+
 // The n%8 leftover elements are copied verbatim behind the last block
 // (src/bitshuffle_core.c:1919-1926); their offset is only known on the device.
 __global__ void k_encode_finish(const uint64_t* offs, int64_t nblocks, const uint8_t* tail_src,
@@ -1140,6 +1199,15 @@ bool lds_layout_ok(const void* fn) {
     return hipFuncGetAttributes(&at, fn) == hipSuccess && at.sharedSizeBytes == 0;
 }
 
+template <bool READBACK>
+hipError_t launch_big_t(const uint8_t* shuf, const Layout& L, const EncodeBufs& b, hipStream_t s) {
+    const int64_t nb = L.nblocks();
+    auto fn = k_lz4_encode_big<READBACK>;
+    ProfScope prof("k_lz4_encode_big", s);
+    hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kWave), kTableBytes, s, shuf, L, b.scratch, b.slot, b.foot);
+    return hipGetLastError();
+}
+
 template <int EK, bool WIDE, int VAR = 0>
 hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s) {
     if constexpr (EK == 2 && !WIDE && VAR == 0) {
@@ -1182,6 +1250,11 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
 }  // namespace
 
 int64_t max_device_block_bytes() { return 160 * 1024 - kTableBytes - 64; }
+
+hipError_t launch_encode_big(const uint8_t* shuf, const Layout& L, const EncodeBufs& b, hipStream_t s) {
+    if (L.nblocks() == 0) return hipSuccess;
+    return lds_atomics_lane_ordered() ? launch_big_t<false>(shuf, L, b, s) : launch_big_t<true>(shuf, L, b, s);
+}
 
 int64_t encode_slot_bytes(const Layout& L) {
     const int64_t n = (int64_t)L.bs * L.E;

@@ -249,6 +249,8 @@ hipError_t launch_encode_large(const uint8_t* in, const Layout& L, const EncodeB
     if (nb == 0) return hipSuccess;
     hipError_t e = launch_transpose(in, shuf, L, true, s);
     if (e != hipSuccess) return e;
+    if (tuning_variant() != 1024) return launch_encode_big(shuf, L, b, s);
+    // A/B variant 1024: the lane-0 parse with the table in global memory
     e = dev_fill(tables, 0, (size_t)nb * kLargeTableWords * 4, s);
     if (e != hipSuccess) return e;
     ProfScope prof("k_lz4_encode_seq", s);
@@ -261,10 +263,15 @@ hipError_t launch_decode_large(const uint8_t* in, int64_t in_nbytes, uint8_t* ou
                                const DecodeBufs& b, uint8_t* shuf, hipStream_t s) {
     const int64_t nb = L.nblocks();
     if (nb == 0) return hipSuccess;
-    ProfScope prof("k_lz4_exec_seq", s);
-    hipLaunchKernelGGL(k_lz4_exec_seq, dim3((unsigned)nb), dim3(64), 0, s, in, in_nbytes, b.offs,
-                       b.status, b.seq, L, shuf, b.bad);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipSuccess;
+    if (tuning_variant() != 1024) {
+        e = launch_exec_big(in, L, b, shuf, s);
+    } else {  // A/B variant 1024: the lane-0 copy loop
+        ProfScope prof("k_lz4_exec_seq", s);
+        hipLaunchKernelGGL(k_lz4_exec_seq, dim3((unsigned)nb), dim3(64), 0, s, in, in_nbytes, b.offs,
+                           b.status, b.seq, L, shuf, b.bad);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess) return e;
     return launch_transpose(shuf, out, L, false, s);
 }

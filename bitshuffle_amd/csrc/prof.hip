@@ -136,8 +136,9 @@ int bshuf_set_variant(int v) {
     // lookup by lane 0's returning exchange, decoder record access 16 global
     // + touch / 32 global / 64 own LDS buffer (default: in place), 128
     // insert/readback search window (the fallback for devices without
-    // lane-ordered LDS atomics)
-    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128) return -71;
+    // lane-ordered LDS atomics), 1024 large blocks by the lane-0 parse
+    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 1024)
+        return -71;
     t_variant = v;
     return 0;
 }
