@@ -1415,7 +1415,7 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
 #undef BSHUF_DEC
     hipError_t e = scan_impl(a, nb, s);
     if (e != hipSuccess) return e;
-#ifdef BSHUF_DIAG
+#if defined(BSHUF_DIAG) || defined(BSHUF_OCC)
     // occupancy experiment: BSHUF_DIAG_DEC_WAVES=w pads the LDS request so
     // that at most w waves fit a CU
     if (const char* w = getenv("BSHUF_DIAG_DEC_WAVES")) {

@@ -160,6 +160,15 @@ struct Table {
     // order (checked on the device before first use: lds_atomics_lane_ordered),
     // so lane j gets the value of the highest LOWER active lane with the same
     // entry, else the table's -- exactly the sequential insert-then-lookup.
+    // exchange() when `doit`, else a read of entry h that changes nothing (a
+    // mask-0 ds_mskor), so every lane can issue it (byU16 only).
+    __device__ __forceinline__ uint32_t exchange_if(uint32_t h, uint32_t v, bool doit) const {
+        static_assert(!WIDE, "byU16 table only");
+        const uint32_t sh = 16u * (h & 1u);
+        const uint32_t old = lds_mskor_rtn(lds_addr(base + 4 * (h >> 1)), doit ? 0xFFFFu << sh : 0u,
+                                           doit ? v << sh : 0u);
+        return (old >> sh) & 0xFFFFu;
+    }
     __device__ __forceinline__ uint32_t exchange(uint32_t h, uint32_t v) const {
         if constexpr (WIDE) {
             return lds_xchg_rtn(lds_addr(base + 4 * h), v);
@@ -379,19 +388,49 @@ __device__ __forceinline__ int window_equal(uint32_t va, uint32_t vb, int lim) {
     return min(c, max(lim, 0));
 }
 
+// Speculative re-test lookups (byU16 table): while a count is still
+// deciding where the match ends, lane j prepares the re-test at ip' = sb + j
+// -- the hashes of ip'-2 and ip' and the table entry for ip' exactly as the
+// sequential parse reads it after inserting ip'-2 (lz4/lz4.c:1230-1236) --
+// so the re-test needs no table round trip of its own once the count is in:
+// one readlane picks lane ip' - sb.  The table read is issued after every
+// insert that precedes it (the parse's volatile LDS ops stay in order), and
+// nothing is inserted between that read and the re-test it serves except
+// ip'-2, which the h2 == h0 select accounts for.
+struct SpecRT {
+    uint32_t x2, x0;  // bytes at ip'-2 and ip' (issued with the count's first window)
+    uint32_t h2, h0, c2;
+    int sb;
+};
+template <class Blk>
+__device__ __forceinline__ void spec_issue(SpecRT& s, const Blk& D, int n, int sb, int lane) {
+    s.sb = sb;
+    s.x2 = lds_rd32(D, min(sb - 2 + lane, n));
+    s.x0 = lds_rd32(D, min(sb + lane, n));
+}
+__device__ __forceinline__ void spec_lookup(SpecRT& s, const Table<false>& T, int lane) {
+    s.h2 = hash4(s.x2);
+    s.h0 = hash4(s.x0);
+    const uint32_t t = T.get(s.h0);
+    s.c2 = s.h2 == s.h0 ? (uint32_t)(s.sb + lane - 2) : t;
+}
+
 // The re-test's match test and LZ4_count in one LDS round trip: counts the
 // equal bytes from ip itself (the first window's lane 0 is the 4-byte
 // test).  cnt = match length beyond kMinMatch, or -1 when there is no match.
-template <class Blk>
+template <bool SPEC = false, class Blk, class TT = Table<false>>
 __device__ __forceinline__ CountOut test_and_count(const Blk& D, int n, int ip, int ref,
-                                                   int mlimit, int lane, uint32_t va0) {
+                                                   int mlimit, int lane, uint32_t va0,
+                                                   const TT* T = nullptr, SpecRT* sp = nullptr) {
     CountOut r;
     r.back = 0;
     uint32_t va = va0, vb = lds_rd32(D, min(ref + 4 * lane, n));  // va0: the a-side, read ahead
+    if constexpr (SPEC) spec_issue(*sp, D, n, ip + kMinMatch, lane);
     if (__builtin_amdgcn_readfirstlane(va ^ vb) != 0) {
         r.cnt = -1;
         return r;
     }
+    if constexpr (SPEC) spec_lookup(*sp, *T, lane);
     for (int total = 0;; total += kWinBytes) {
         const int c = window_equal(va, vb, mlimit - (ip + total));
         if (c < kWinBytes) {
@@ -405,15 +444,20 @@ __device__ __forceinline__ CountOut test_and_count(const Blk& D, int n, int ip, 
     }
 }
 
-template <class Blk>
+template <bool SPEC = false, class Blk, class TT = Table<false>>
 __device__ __forceinline__ CountOut catch_and_count(const Blk& D, int n, int ip, int ref,
-                                                    int anchor, int mlimit, int lane) {
+                                                    int anchor, int mlimit, int lane,
+                                                    const TT* T = nullptr, SpecRT* sp = nullptr) {
     CountOut r;
     // first forward window and backward bytes together
     const int a = ip + kMinMatch, b = ref + kMinMatch;
     uint32_t va = lds_rd32(D, min(a + 4 * lane, n)), vb = lds_rd32(D, min(b + 4 * lane, n));
     const int ba = ip - 1 - lane, bb = ref - 1 - lane;
     const uint32_t ca = (uint32_t)D[max(ba, 0)], cb = (uint32_t)D[max(bb, 0)];
+    if constexpr (SPEC) {
+        spec_issue(*sp, D, n, a, lane);
+        spec_lookup(*sp, *T, lane);
+    }
     // backward
     {
         uint64_t cm = ballot(ba >= anchor && bb >= 0 && ca == cb);
@@ -514,12 +558,16 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                         // insert-then-lookup; candidate bytes come from the
                         // (immutable) block in LDS
                         uint32_t h = 0, cand = 0;
-                        if (valid) {
-                            if constexpr (WIDE)
+                        if constexpr (WIDE) {
+                            if (valid) {
                                 h = hash5(lds_rd64(D, pos));
-                            else
-                                h = hash4(seq);
-                            cand = T.exchange(h, (uint32_t)pos);
+                                cand = T.exchange(h, (uint32_t)pos);
+                            }
+                        } else {
+                            // no exec-mask switch: a lane past mflimit runs a
+                            // mask-0 exchange (reads its entry, changes nothing)
+                            h = hash4(seq);
+                            cand = T.exchange_if(h, (uint32_t)pos, valid);
                         }
                         const uint32_t dcand = lds_rd32(D, (int)cand);
                         // the compare's own mask, and-ed with the valid lanes on the
@@ -606,7 +654,10 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
             if (mpos < 0) break;
             COUNT(0, 1);
             // ------------------------------------------------ catch up + count
-            CountOut co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
+            // speculative re-test lookups (default; A/B variant 2048 turns them off)
+            constexpr bool kSpec = !WIDE && (OPT & 2048) == 0;
+            SpecRT sp;
+            CountOut co = catch_and_count<kSpec>(D, n, mpos, mref, anchor, mlimit, lane, &T, &sp);
             ip = mpos - co.back;
             int ref = mref - co.back;
             int mc = co.back + co.cnt;
@@ -620,6 +671,29 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 STAMP(3);
                 if (ip >= limit) break;
                 // fill table at ip-2, then test ip (lz4/lz4.c:1230-1293)
+                if constexpr (kSpec) {
+                    const int j = ip - sp.sb;
+                    if (j < kWave) {
+                        // the count's shadow already did the table read
+                        const uint32_t c2 = (uint32_t)__builtin_amdgcn_readlane((int)sp.c2, j);
+                        const uint32_t h2 = (uint32_t)__builtin_amdgcn_readlane((int)sp.h2, j);
+                        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)sp.h0, j);
+                        pre = lds_rd32(D, min(ip + 1 + lane, n));
+                        const uint32_t va0 = lds_rd32(D, min(ip + 4 * lane, n));
+                        T.put(h2, (uint32_t)(ip - 2));
+                        T.put(h0, (uint32_t)ip);
+                        co = test_and_count<kSpec>(D, n, ip, (int)c2, mlimit, lane, va0, &T, &sp);
+                        if (co.cnt >= 0) {
+                            ref = (int)c2;
+                            mc = co.cnt;
+                            COUNT(3, 1);
+                            STAMP(4);
+                            continue;
+                        }
+                        STAMP(4);
+                        break;
+                    }
+                }
                 const int t = ip - co.tail_base;
                 uint32_t x2, x0, h2, h0;
                 if (!WIDE && t >= 2 && t <= 4 * kWave - 8) {
@@ -655,7 +729,7 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 }
                 const bool near = !WIDE || c2 + kMaxDistance >= (uint32_t)ip;
                 if (near) {
-                    co = test_and_count(D, n, ip, (int)c2, mlimit, lane, va0);
+                    co = test_and_count<kSpec>(D, n, ip, (int)c2, mlimit, lane, va0, &T, &sp);
                     if (co.cnt >= 0) {
                         // zero-literal sequence, no catch-up on this path
                         ref = (int)c2;
@@ -843,6 +917,19 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if (raw_fits(m0)) issue_raw_loads(RW, blk_src(blk), m0 * E, lane);
     }
 
+    // Deferred copy-out (EK != 0; A/B variant 4096 turns it off): a block's
+    // record stays in the table's LDS until the next block is transposed.
+    constexpr bool kDefer = EK != 0 && (VAR & 4096) == 0;
+    int64_t pend_blk = -1;
+    int pend_c = 0;
+    auto flush_pending = [&]() {
+        if (pend_blk < 0) return;
+        uint8_t* po = a.scratch + pend_blk * a.slot;
+        const int nch = (4 + pend_c + 15) >> 4;
+        for (int i = lane; i < nch; i += kWave) ((gbl128*)po)[i] = ((const lds128*)L0)[i];
+        if (lane == 0) a.foot[pend_blk] = 4 + (uint64_t)pend_c;
+        pend_blk = -1;
+    };
     KDIAG_DECL
     for (;;) {
         KSTAMP(3);
@@ -877,8 +964,12 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
             }
         }
         // zero the hash table (LZ4_initStream) and the read pad behind the block
-        for (int i = lane; i < kTableBytes / 16; i += kWave)
-            ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
+        // (deferred copy-out: after the transpose, once the previous record
+        // has left the table's LDS)
+        if constexpr (!kDefer) {
+            for (int i = lane; i < kTableBytes / 16; i += kWave)
+                ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
+        }
         if (lane < kDataPad / 4) ((lds32*)(D + ((n + 3) & ~3)))[lane] = 0;
         // bit transpose into LDS (bshuf_trans_bit_elem)
         if (staged) {
@@ -912,6 +1003,17 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        if constexpr (kDefer) {
+            // the previous block's record leaves now, behind this block's
+            // transpose: its stores are older than the prefetch below, so the
+            // next iteration's wait for that prefetch finds them long done
+            // (issued at the end of a parse, they would hold it up instead)
+            flush_pending();
+            for (int i = lane; i < kTableBytes / 16; i += kWave)
+                ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
         // prefetch the next block while this one is parsed
         const int64_t next = blk + stride;
         if constexpr (EK != 0) {
@@ -939,7 +1041,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if constexpr (kDesc) {
             if (a.desc_ok && 4 + lz4_bound(n) + 15 <= kTableBytes) {
                 EmitDesc em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback, (VAR & 8)>(D, n, T, em, lane);
+                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 2048))>(D, n, T, em, lane);
                 KSTAMP(1);
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -949,9 +1051,14 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                     if (lane < 4) S[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
-                    const int nch = (4 + c + 15) >> 4;
-                    for (int i = lane; i < nch; i += kWave)
-                        ((gbl128*)out)[i] = ((const lds128*)S)[i];
+                    if constexpr (kDefer) {
+                        pend_blk = blk;
+                        pend_c = c;
+                    } else {
+                        const int nch = (4 + c + 15) >> 4;
+                        for (int i = lane; i < nch; i += kWave)
+                            ((gbl128*)out)[i] = ((const lds128*)S)[i];
+                    }
                 } else {
                     // more sequences than descriptor slots: parse again with
                     // the inline emitter (fresh table)
@@ -964,16 +1071,17 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         }
         if (c < 0) {
             EmitBytes<> em{out + 4, D, lane};
-            c = lz4_encode_block<WIDE, kReadback, (VAR & 8)>(D, n, T, em, lane);
+            c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 2048))>(D, n, T, em, lane);
             if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         }
-        if (lane == 0) a.foot[blk] = 4 + (uint64_t)c;
+        if (lane == 0 && pend_blk != blk) a.foot[blk] = 4 + (uint64_t)c;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         KSTAMP(2);
         if (next >= nb) break;
         blk = next;
     }
+    if constexpr (kDefer) flush_pending();
     KDIAG_FLUSH;
 }
 
@@ -1218,6 +1326,8 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 4) return launch_enc_t<2, false, 4>(a, nb, lds, s);
         if (v == 128) return launch_enc_t<2, false, 128>(a, nb, lds, s);
         if (v == 8) return launch_enc_t<2, false, 8>(a, nb, lds, s);
+        if (v == 2048) return launch_enc_t<2, false, 2048>(a, nb, lds, s);
+        if (v == 4096) return launch_enc_t<2, false, 4096>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
@@ -1229,7 +1339,7 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-#ifdef BSHUF_DIAG
+#if defined(BSHUF_DIAG) || defined(BSHUF_OCC)
     // occupancy experiment: BSHUF_DIAG_WAVES=w pads the LDS request so that at
     // most w waves fit a CU
     if (const char* w = getenv("BSHUF_DIAG_WAVES")) {

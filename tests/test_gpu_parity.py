@@ -136,7 +136,7 @@ def test_variant_knob_rejects_ablations(bs):
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 2048, 4096])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
@@ -146,7 +146,10 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     every lane); decoder record access: 16 straight from global memory with
     each record's lines touched two blocks ahead, 32 the same without the
     touch, 64 staged in an LDS buffer of its own (the default decodes each
-    record in place at the end of its block's LDS buffer)."""
+    record in place at the end of its block's LDS buffer); 2048 the re-test's
+    table lookup on the chain (the default does it speculatively in the
+    shadow of the count); 4096 each record copied out at the end of its own
+    block (the default defers it behind the next block's transpose)."""
     rng = np.random.default_rng(128)
     cases = [oracle.gen_g1(3 * 4096 + 1005),
              (rng.integers(-2, 3, 50000).cumsum() % 97).astype(np.int16),

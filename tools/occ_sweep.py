@@ -7,7 +7,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["BSHUF_LIB"] = os.path.join(ROOT, "bitshuffle_amd", "libbitshuffle_mi355x_diag.so")
+os.environ.setdefault("BSHUF_LIB", os.path.join(ROOT, "bitshuffle_amd", "libbitshuffle_mi355x_diag.so"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import bitshuffle_amd as B  # noqa: E402
