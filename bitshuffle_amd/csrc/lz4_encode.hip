@@ -160,15 +160,6 @@ struct Table {
     // order (checked on the device before first use: lds_atomics_lane_ordered),
     // so lane j gets the value of the highest LOWER active lane with the same
     // entry, else the table's -- exactly the sequential insert-then-lookup.
-    // exchange() when `doit`, else a read of entry h that changes nothing (a
-    // mask-0 ds_mskor), so every lane can issue it (byU16 only).
-    __device__ __forceinline__ uint32_t exchange_if(uint32_t h, uint32_t v, bool doit) const {
-        static_assert(!WIDE, "byU16 table only");
-        const uint32_t sh = 16u * (h & 1u);
-        const uint32_t old = lds_mskor_rtn(lds_addr(base + 4 * (h >> 1)), doit ? 0xFFFFu << sh : 0u,
-                                           doit ? v << sh : 0u);
-        return (old >> sh) & 0xFFFFu;
-    }
     __device__ __forceinline__ uint32_t exchange(uint32_t h, uint32_t v) const {
         if constexpr (WIDE) {
             return lds_xchg_rtn(lds_addr(base + 4 * h), v);
@@ -204,6 +195,16 @@ __device__ __forceinline__ uint64_t lds_rd64(const GblBlk& D, int p) {
 }
 __device__ __forceinline__ uint32_t blk_w32(const lds8* D, int a) { return *(const lds32*)(D + a); }
 __device__ __forceinline__ uint32_t blk_w32(const GblBlk& D, int a) { return D.w32(a); }
+
+// A count / re-test window read at p (p < n + 260).  An LDS block is followed
+// by >= 2 KiB of readable LDS (pad + descriptors), whose bytes never decide
+// anything (every count is capped at mlimit), so it needs no clamp; the
+// global-memory block's scratch is padded by only 12 bytes.
+__device__ __forceinline__ uint32_t rdw(const lds8* D, int p, int n) {
+    (void)n;
+    return lds_rd32(D, p);
+}
+__device__ __forceinline__ uint32_t rdw(const GblBlk& D, int p, int n) { return lds_rd32(D, min(p, n)); }
 
 template <bool WIDE, class Blk>
 __device__ __forceinline__ uint32_t hash_at(const Blk& D, int p) {
@@ -388,49 +389,19 @@ __device__ __forceinline__ int window_equal(uint32_t va, uint32_t vb, int lim) {
     return min(c, max(lim, 0));
 }
 
-// Speculative re-test lookups (byU16 table): while a count is still
-// deciding where the match ends, lane j prepares the re-test at ip' = sb + j
-// -- the hashes of ip'-2 and ip' and the table entry for ip' exactly as the
-// sequential parse reads it after inserting ip'-2 (lz4/lz4.c:1230-1236) --
-// so the re-test needs no table round trip of its own once the count is in:
-// one readlane picks lane ip' - sb.  The table read is issued after every
-// insert that precedes it (the parse's volatile LDS ops stay in order), and
-// nothing is inserted between that read and the re-test it serves except
-// ip'-2, which the h2 == h0 select accounts for.
-struct SpecRT {
-    uint32_t x2, x0;  // bytes at ip'-2 and ip' (issued with the count's first window)
-    uint32_t h2, h0, c2;
-    int sb;
-};
-template <class Blk>
-__device__ __forceinline__ void spec_issue(SpecRT& s, const Blk& D, int n, int sb, int lane) {
-    s.sb = sb;
-    s.x2 = lds_rd32(D, min(sb - 2 + lane, n));
-    s.x0 = lds_rd32(D, min(sb + lane, n));
-}
-__device__ __forceinline__ void spec_lookup(SpecRT& s, const Table<false>& T, int lane) {
-    s.h2 = hash4(s.x2);
-    s.h0 = hash4(s.x0);
-    const uint32_t t = T.get(s.h0);
-    s.c2 = s.h2 == s.h0 ? (uint32_t)(s.sb + lane - 2) : t;
-}
-
 // The re-test's match test and LZ4_count in one LDS round trip: counts the
 // equal bytes from ip itself (the first window's lane 0 is the 4-byte
 // test).  cnt = match length beyond kMinMatch, or -1 when there is no match.
-template <bool SPEC = false, class Blk, class TT = Table<false>>
+template <class Blk>
 __device__ __forceinline__ CountOut test_and_count(const Blk& D, int n, int ip, int ref,
-                                                   int mlimit, int lane, uint32_t va0,
-                                                   const TT* T = nullptr, SpecRT* sp = nullptr) {
+                                                   int mlimit, int lane, uint32_t va0) {
     CountOut r;
     r.back = 0;
-    uint32_t va = va0, vb = lds_rd32(D, min(ref + 4 * lane, n));  // va0: the a-side, read ahead
-    if constexpr (SPEC) spec_issue(*sp, D, n, ip + kMinMatch, lane);
+    uint32_t va = va0, vb = rdw(D, ref + 4 * lane, n);  // va0: the a-side, read ahead
     if (__builtin_amdgcn_readfirstlane(va ^ vb) != 0) {
         r.cnt = -1;
         return r;
     }
-    if constexpr (SPEC) spec_lookup(*sp, *T, lane);
     for (int total = 0;; total += kWinBytes) {
         const int c = window_equal(va, vb, mlimit - (ip + total));
         if (c < kWinBytes) {
@@ -439,25 +410,20 @@ __device__ __forceinline__ CountOut test_and_count(const Blk& D, int n, int ip, 
             r.tail = va;
             return r;
         }
-        va = lds_rd32(D, min(ip + total + kWinBytes + 4 * lane, n));
-        vb = lds_rd32(D, min(ref + total + kWinBytes + 4 * lane, n));
+        va = rdw(D, ip + total + kWinBytes + 4 * lane, n);
+        vb = rdw(D, ref + total + kWinBytes + 4 * lane, n);
     }
 }
 
-template <bool SPEC = false, class Blk, class TT = Table<false>>
+template <class Blk>
 __device__ __forceinline__ CountOut catch_and_count(const Blk& D, int n, int ip, int ref,
-                                                    int anchor, int mlimit, int lane,
-                                                    const TT* T = nullptr, SpecRT* sp = nullptr) {
+                                                    int anchor, int mlimit, int lane) {
     CountOut r;
     // first forward window and backward bytes together
     const int a = ip + kMinMatch, b = ref + kMinMatch;
-    uint32_t va = lds_rd32(D, min(a + 4 * lane, n)), vb = lds_rd32(D, min(b + 4 * lane, n));
+    uint32_t va = rdw(D, a + 4 * lane, n), vb = rdw(D, b + 4 * lane, n);
     const int ba = ip - 1 - lane, bb = ref - 1 - lane;
     const uint32_t ca = (uint32_t)D[max(ba, 0)], cb = (uint32_t)D[max(bb, 0)];
-    if constexpr (SPEC) {
-        spec_issue(*sp, D, n, a, lane);
-        spec_lookup(*sp, *T, lane);
-    }
     // backward
     {
         uint64_t cm = ballot(ba >= anchor && bb >= 0 && ca == cb);
@@ -482,8 +448,8 @@ __device__ __forceinline__ CountOut catch_and_count(const Blk& D, int n, int ip,
             r.tail = va;
             return r;
         }
-        va = lds_rd32(D, min(a + total + kWinBytes + 4 * lane, n));
-        vb = lds_rd32(D, min(b + total + kWinBytes + 4 * lane, n));
+        va = rdw(D, a + total + kWinBytes + 4 * lane, n);
+        vb = rdw(D, b + total + kWinBytes + 4 * lane, n);
     }
 }
 
@@ -558,16 +524,12 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                         // insert-then-lookup; candidate bytes come from the
                         // (immutable) block in LDS
                         uint32_t h = 0, cand = 0;
-                        if constexpr (WIDE) {
-                            if (valid) {
+                        if (valid) {
+                            if constexpr (WIDE)
                                 h = hash5(lds_rd64(D, pos));
-                                cand = T.exchange(h, (uint32_t)pos);
-                            }
-                        } else {
-                            // no exec-mask switch: a lane past mflimit runs a
-                            // mask-0 exchange (reads its entry, changes nothing)
-                            h = hash4(seq);
-                            cand = T.exchange_if(h, (uint32_t)pos, valid);
+                            else
+                                h = hash4(seq);
+                            cand = T.exchange(h, (uint32_t)pos);
                         }
                         const uint32_t dcand = lds_rd32(D, (int)cand);
                         // the compare's own mask, and-ed with the valid lanes on the
@@ -654,10 +616,7 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
             if (mpos < 0) break;
             COUNT(0, 1);
             // ------------------------------------------------ catch up + count
-            // speculative re-test lookups (default; A/B variant 2048 turns them off)
-            constexpr bool kSpec = !WIDE && (OPT & 2048) == 0;
-            SpecRT sp;
-            CountOut co = catch_and_count<kSpec>(D, n, mpos, mref, anchor, mlimit, lane, &T, &sp);
+            CountOut co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
             ip = mpos - co.back;
             int ref = mref - co.back;
             int mc = co.back + co.cnt;
@@ -671,29 +630,6 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 STAMP(3);
                 if (ip >= limit) break;
                 // fill table at ip-2, then test ip (lz4/lz4.c:1230-1293)
-                if constexpr (kSpec) {
-                    const int j = ip - sp.sb;
-                    if (j < kWave) {
-                        // the count's shadow already did the table read
-                        const uint32_t c2 = (uint32_t)__builtin_amdgcn_readlane((int)sp.c2, j);
-                        const uint32_t h2 = (uint32_t)__builtin_amdgcn_readlane((int)sp.h2, j);
-                        const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)sp.h0, j);
-                        pre = lds_rd32(D, min(ip + 1 + lane, n));
-                        const uint32_t va0 = lds_rd32(D, min(ip + 4 * lane, n));
-                        T.put(h2, (uint32_t)(ip - 2));
-                        T.put(h0, (uint32_t)ip);
-                        co = test_and_count<kSpec>(D, n, ip, (int)c2, mlimit, lane, va0, &T, &sp);
-                        if (co.cnt >= 0) {
-                            ref = (int)c2;
-                            mc = co.cnt;
-                            COUNT(3, 1);
-                            STAMP(4);
-                            continue;
-                        }
-                        STAMP(4);
-                        break;
-                    }
-                }
                 const int t = ip - co.tail_base;
                 uint32_t x2, x0, h2, h0;
                 if (!WIDE && t >= 2 && t <= 4 * kWave - 8) {
@@ -708,8 +644,8 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 }
                 // the next search window's bytes and the test's a-side window,
                 // in flight during the table exchange
-                pre = lds_rd32(D, min(ip + 1 + lane, n));
-                const uint32_t va0 = lds_rd32(D, min(ip + 4 * lane, n));
+                pre = rdw(D, ip + 1 + lane, n);
+                const uint32_t va0 = rdw(D, ip + 4 * lane, n);
                 uint32_t c2 = 0;
                 if constexpr ((OPT & 8) == 0) {
                     // plain ops by every lane (same address, same value; the
@@ -727,9 +663,42 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                     }
                     c2 = uni(c2);
                 }
+                if constexpr (!WIDE && (OPT & 2048) == 0) {
+                    // the 4-byte test is lane 0's bit of the count's first
+                    // ballot (no separate readfirstlane compare); A/B variant
+                    // 2048: test_and_count
+                    uint32_t va = va0, vb = rdw(D, (int)c2 + 4 * lane, n);
+                    uint64_t ne = ballot(va != vb);
+                    if (ne & 1ull) {
+                        STAMP(4);
+                        break;
+                    }
+                    int total = 0, c;
+                    for (;;) {
+                        c = kWinBytes;
+                        if (ne) {
+                            const int f = ffs64(ne);
+                            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)(va ^ vb), f);
+                            c = 4 * f + (__builtin_ctz(x) >> 3);
+                        }
+                        c = min(c, max(mlimit - (ip + total), 0));
+                        if (c < kWinBytes) break;
+                        total += kWinBytes;
+                        va = rdw(D, ip + total + 4 * lane, n);
+                        vb = rdw(D, (int)c2 + total + 4 * lane, n);
+                        ne = ballot(va != vb);
+                    }
+                    co.tail = va;
+                    co.tail_base = ip + total;
+                    ref = (int)c2;
+                    mc = total + c - kMinMatch;
+                    COUNT(3, 1);
+                    STAMP(4);
+                    continue;
+                }
                 const bool near = !WIDE || c2 + kMaxDistance >= (uint32_t)ip;
                 if (near) {
-                    co = test_and_count<kSpec>(D, n, ip, (int)c2, mlimit, lane, va0, &T, &sp);
+                    co = test_and_count(D, n, ip, (int)c2, mlimit, lane, va0);
                     if (co.cnt >= 0) {
                         // zero-literal sequence, no catch-up on this path
                         ref = (int)c2;
@@ -1326,8 +1295,8 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 4) return launch_enc_t<2, false, 4>(a, nb, lds, s);
         if (v == 128) return launch_enc_t<2, false, 128>(a, nb, lds, s);
         if (v == 8) return launch_enc_t<2, false, 8>(a, nb, lds, s);
-        if (v == 2048) return launch_enc_t<2, false, 2048>(a, nb, lds, s);
         if (v == 4096) return launch_enc_t<2, false, 4096>(a, nb, lds, s);
+        if (v == 2048) return launch_enc_t<2, false, 2048>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);

@@ -137,7 +137,7 @@ int bshuf_set_variant(int v) {
     // + touch / 32 global / 64 own LDS buffer (default: in place), 128
     // insert/readback search window (the fallback for devices without
     // lane-ordered LDS atomics), 1024 large blocks by the lane-0 parse, 2048
-    // re-test table lookups on the chain (no speculative lookups), 4096 record
+    // the re-test's 4-byte test by readfirstlane before the count, 4096 record
     // copy-out at the end of its block's parse (not deferred)
     if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 1024 && v != 2048 && v != 4096)
         return -71;

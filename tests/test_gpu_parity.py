@@ -147,9 +147,9 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     each record's lines touched two blocks ahead, 32 the same without the
     touch, 64 staged in an LDS buffer of its own (the default decodes each
     record in place at the end of its block's LDS buffer); 2048 the re-test's
-    table lookup on the chain (the default does it speculatively in the
-    shadow of the count); 4096 each record copied out at the end of its own
-    block (the default defers it behind the next block's transpose)."""
+    4-byte test as its own readfirstlane compare before the count; 4096 each record
+    copied out at the end of its own block (the default defers it behind the
+    next block's transpose)."""
     rng = np.random.default_rng(128)
     cases = [oracle.gen_g1(3 * 4096 + 1005),
              (rng.integers(-2, 3, 50000).cumsum() % 97).astype(np.int16),
