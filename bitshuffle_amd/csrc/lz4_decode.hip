@@ -310,6 +310,26 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
         for (int i = lane; i < ml; i += kWave) D[mop + i] = D[s + small_mod(i, off, rinv)];
         return;
     }
+    if (off == 1 || off == 2 || off == 4) {
+        // period dividing 4 (offset 2 is 40 % of the matches of bit-shuffled
+        // int16 data): every aligned dword of the fill is the same rotated
+        // pattern dword
+        const uint32_t b0 = D[s], b1 = D[s + (off > 1 ? 1 : 0)], b2 = D[s + (off > 2 ? 2 : 0)],
+                       b3 = D[s + (off > 2 ? 3 : off - 1)];
+        const uint32_t v = off == 1 ? b0 * 0x01010101u
+                         : off == 2 ? (b0 | (b1 << 8)) * 0x00010001u
+                                    : (b0 | (b1 << 8) | (b2 << 16) | (b3 << 24));
+        const int head = q0 - mop, tailn = mop + ml - q1;
+        const uint32_t rot = 8u * (uint32_t)(head & (off - 1));
+        const uint32_t w = rot ? (v >> rot) | (v << (32u - rot)) : v;
+        const int e = lane < 4 ? lane : ml - tailn + (lane - 4);
+        if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn))
+            D[mop + e] = (uint8_t)(v >> (8 * (e & (off - 1))));
+        const int nw = (q1 - q0) >> 2;
+        lds32* W = (lds32*)(D + q0);
+        for (int c = lane; c < nw; c += kWave) W[c] = w;
+        return;
+    }
     // <= 3 head and <= 3 tail bytes, then the aligned interior dwords
     const int head = q0 - mop, tailn = mop + ml - q1;
     const int e = lane < 4 ? lane : ml - tailn + (lane - 4);
@@ -412,7 +432,7 @@ __device__ __forceinline__ int read_ext(const Src& Cb, int& q, uint64_t w, int a
 // Phase 2 for one block.  The record payload starts at byte cp of the
 // 4-aligned LDS buffer Cb; pos[0..nseq) are its token positions (payload-
 // relative, validated by the scan); pos0 is this lane's prefetched pos[lane].
-template <bool kInPlace = false, class Src>
+template <bool kInPlace = false, int ABL = 0, class Src>
 __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8* D,
                                const uint32_t* __restrict__ pos, const int nseq, uint32_t pos0,
                                const int lane) {
@@ -450,7 +470,10 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
         const int op = opb + incl - len;
         opb += __builtin_amdgcn_readlane(incl, kWave - 1);
         // ---- literals: short runs per lane, long runs by the whole wave
-        if constexpr (!kInPlace) {
+        // (ABL: diagnostic-build timing ablations -- 1 no literal copies, 2
+        // no match copies; wrong output)
+        if constexpr ((ABL & 1) != 0) {
+        } else if constexpr (!kInPlace) {
             if (lit > 0 && lit <= 16) Cb.copy16(lsrc, D, op, lit);
             for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
                 const int l = ffs64(lm);
@@ -481,11 +504,16 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
         }
         // ---- matches, in batches of mutually independent sequences
         const int mop = op + lit;
-        uint64_t todo = ballot(ml > 0);
+        uint64_t todo = (ABL & 2) ? 0ull : ballot(ml > 0);
         while (todo) {
             const int f = ffs64(todo);
             const int opf = __builtin_amdgcn_readlane(mop, f);
-            const bool stop = lane > f && ml > 0 && (off < ml || mop - off + ml > opf);
+            // a later sequence joins the batch when the bytes its match reads
+            // from before its own output ([mop - off, mop - off + min(ml, off)):
+            // a self-overlapping match makes the rest itself) were all final
+            // before the batch started; self-overlapping and long matches run
+            // one after another by the wave (coop), short ones per lane
+            const bool stop = lane > f && ml > 0 && mop - off + min(ml, off) > opf;
             const uint64_t sm = ballot(stop);
             const int g = sm ? ffs64(sm) : kWave;
             const bool inb = lane >= f && lane < g && ml > 0;
@@ -980,7 +1008,7 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
             const int mx = (int)((cur.scan >> 32) & 0xFFFF) - kMxBias;
             if (!kIP || mx <= (int)(CB - D) + cp + 4) {
                 if (!(VAR & 64))
-                    lz4_exec_block<kIP>(LdsRec{CB}, cp + 4, D, cur.loc.seq + cur.o0 / 3,
+                    lz4_exec_block<kIP, (VAR >> 10) & 3>(LdsRec{CB}, cp + 4, D, cur.loc.seq + cur.o0 / 3,
                                         (int)cur.scan, cur_pos, lane);
             } else {
                 // too little room to decode in place: the record from L2
@@ -1399,6 +1427,8 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
             if (diag_variant() == 8) fn = BSHUF_DEC(2, 520);
             if (diag_variant() == 64) fn = BSHUF_DEC(2, 576);
             if (diag_variant() == 72) fn = BSHUF_DEC(2, 584);
+            if (diag_variant() == 1024) fn = BSHUF_DEC(2, 1536);
+            if (diag_variant() == 2048) fn = BSHUF_DEC(2, 2560);
 #endif
             break;
         case 4:

@@ -1,12 +1,12 @@
 """Decoder time split from the diagnostic build's ablations (wrong output,
 timing only): 0 full, 8 no inverse transpose/stores, 64 no sequence
-execution, 72 neither.  Usage: python tools/diag_decode.py [GiB] [gen]"""
+execution, 72 neither, 1024 no literal copies, 2048 no match copies.  Usage: python tools/diag_decode.py [GiB] [gen]"""
 import ctypes
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["BSHUF_LIB"] = os.path.join(ROOT, "bitshuffle_amd", "libbitshuffle_mi355x_diag.so")
+os.environ.setdefault("BSHUF_LIB", os.path.join(ROOT, "bitshuffle_amd", "libbitshuffle_mi355x_diag.so"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import bitshuffle_amd as B  # noqa: E402
@@ -21,7 +21,7 @@ B.synth_fill_dev(x, gen)
 c = api.compress_lz4_dev(x)
 abl = B.lib.bshuf_diag_set_ablation
 abl.argtypes = [ctypes.c_int]
-for v in (0, 8, 64, 72, 0):
+for v in (0, 8, 64, 72, 1024, 2048, 0):
     abl(v)
     y, r = api.decompress_lz4_dev(c, x.shape, x.dtype, sync=False)
     torch.cuda.synchronize()
