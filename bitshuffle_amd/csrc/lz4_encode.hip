@@ -160,6 +160,15 @@ struct Table {
     // order (checked on the device before first use: lds_atomics_lane_ordered),
     // so lane j gets the value of the highest LOWER active lane with the same
     // entry, else the table's -- exactly the sequential insert-then-lookup.
+    // exchange() when `doit`, else a read of entry h that changes nothing (a
+    // mask-0 ds_mskor): every lane can issue it, no exec-mask switch (byU16)
+    __device__ __forceinline__ uint32_t exchange_if(uint32_t h, uint32_t v, bool doit) const {
+        static_assert(!WIDE, "byU16 table only");
+        const uint32_t sh = 16u * (h & 1u);
+        const uint32_t old = lds_mskor_rtn(lds_addr(base + 4 * (h >> 1)), doit ? 0xFFFFu << sh : 0u,
+                                           doit ? v << sh : 0u);
+        return (old >> sh) & 0xFFFFu;
+    }
     __device__ __forceinline__ uint32_t exchange(uint32_t h, uint32_t v) const {
         if constexpr (WIDE) {
             return lds_xchg_rtn(lds_addr(base + 4 * h), v);
@@ -506,7 +515,57 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 // (the closed form's value, which is 1 for k = 0: `bias`)
                 ProbeLane q0 = probe_lane(lane), q1 = probe_lane(lane + 1);
                 int bias = lane == 0 ? 1 : 0;
-                for (int k0 = 0;; k0 += kWave) {
+                if constexpr (!READBACK && !WIDE && (OPT & 512) == 0) {
+                    // full windows (every probe and its successor inside
+                    // mflimit) are told by the last lane's successor offset,
+                    // kept on the scalar unit: no validity ballot, no masks;
+                    // the one partial window at the end takes the general
+                    // path below.  A/B variant 512: every window general.
+                    ProbeLane qs = probe_lane(kWave);
+                    int k0 = 0;
+                    for (; p0 + qs.off <= limit; k0 += kWave) {
+                        COUNT(1, 1);
+                        const int pos = p0 + q0.off - bias;
+                        const int pos_n = p0 + q0.off + q0.step;
+                        q0.advance();
+                        qs.advance();
+                        bias = 0;
+                        const uint32_t seq_nxt = lds_rd32(D, min(pos_n, n));
+                        const uint32_t h = hash4(seq_cur);
+                        const uint32_t cand = T.exchange(h, (uint32_t)pos);
+                        const uint32_t dcand = lds_rd32(D, (int)cand);
+                        const uint64_t mm = ballot(dcand == seq_cur);
+                        if (mm) {
+                            const int js = ffs64(mm);
+                            mpos = __builtin_amdgcn_readlane(pos, js);
+                            if (lane > js && cand <= (uint32_t)mpos) T.put(h, cand);
+                            mref = __builtin_amdgcn_readlane((int)cand, js);
+                            break;
+                        }
+                        seq_cur = seq_nxt;
+                    }
+                    if (mpos < 0) {
+                        // the partial window (if any probe of it is valid)
+                        q1 = probe_lane(k0 + lane + 1);
+                        const int pos = p0 + q0.off - bias;
+                        const bool valid = p0 + q1.off <= limit;
+                        const uint64_t vmask = ballot(valid);
+                        if (vmask != 0) {
+                            COUNT(1, 1);
+                            const uint32_t h = hash4(seq_cur);
+                            const uint32_t cand = T.exchange_if(h, (uint32_t)pos, valid);
+                            const uint32_t dcand = lds_rd32(D, (int)cand);
+                            const uint64_t mm = vmask & ballot(dcand == seq_cur);
+                            if (mm) {
+                                const int js = ffs64(mm);
+                                mpos = __builtin_amdgcn_readlane(pos, js);
+                                if (valid && lane > js && cand <= (uint32_t)mpos) T.put(h, cand);
+                                mref = __builtin_amdgcn_readlane((int)cand, js);
+                            }
+                        }
+                    }
+                }
+                for (int k0 = 0; READBACK || WIDE || (OPT & 512) != 0; k0 += kWave) {
                     COUNT(1, 1);
                     const int pos = p0 + q0.off - bias;
                     const bool valid = p0 + q1.off <= limit;
@@ -1010,7 +1069,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if constexpr (kDesc) {
             if (a.desc_ok && 4 + lz4_bound(n) + 15 <= kTableBytes) {
                 EmitDesc em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 2048))>(D, n, T, em, lane);
+                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048))>(D, n, T, em, lane);
                 KSTAMP(1);
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1040,7 +1099,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         }
         if (c < 0) {
             EmitBytes<> em{out + 4, D, lane};
-            c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 2048))>(D, n, T, em, lane);
+            c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048))>(D, n, T, em, lane);
             if (lane < 4) out[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
         }
         if (lane == 0 && pend_blk != blk) a.foot[blk] = 4 + (uint64_t)c;
@@ -1297,6 +1356,7 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 8) return launch_enc_t<2, false, 8>(a, nb, lds, s);
         if (v == 4096) return launch_enc_t<2, false, 4096>(a, nb, lds, s);
         if (v == 2048) return launch_enc_t<2, false, 2048>(a, nb, lds, s);
+        if (v == 512) return launch_enc_t<2, false, 512>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);

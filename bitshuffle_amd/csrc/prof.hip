@@ -136,10 +136,11 @@ int bshuf_set_variant(int v) {
     // lookup by lane 0's returning exchange, decoder record access 16 global
     // + touch / 32 global / 64 own LDS buffer (default: in place), 128
     // insert/readback search window (the fallback for devices without
-    // lane-ordered LDS atomics), 1024 large blocks by the lane-0 parse, 2048
+    // lane-ordered LDS atomics), 512 every search window with per-lane validity
+    // masks, 1024 large blocks by the lane-0 parse, 2048
     // the re-test's 4-byte test by readfirstlane before the count, 4096 record
     // copy-out at the end of its block's parse (not deferred)
-    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 1024 && v != 2048 && v != 4096)
+    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 512 && v != 1024 && v != 2048 && v != 4096)
         return -71;
     t_variant = v;
     return 0;

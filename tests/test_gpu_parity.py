@@ -131,12 +131,12 @@ def _with_variant(bs, variant, fn):
 def test_variant_knob_rejects_ablations(bs):
     """Only byte-identical variants are accepted (and only for the calling
     thread); timing ablations are not in the product library."""
-    for v in (1, 48, 68, 3, -1, 512):
+    for v in (1, 48, 68, 3, -1, 576):
         assert bs.lib.bshuf_set_variant(v) == -71
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 2048, 4096])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
@@ -146,7 +146,9 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     every lane); decoder record access: 16 straight from global memory with
     each record's lines touched two blocks ahead, 32 the same without the
     touch, 64 staged in an LDS buffer of its own (the default decodes each
-    record in place at the end of its block's LDS buffer); 2048 the re-test's
+    record in place at the end of its block's LDS buffer); 512 every search
+    window with per-lane validity masks (the default runs full windows
+    without them); 2048 the re-test's
     4-byte test as its own readfirstlane compare before the count; 4096 each record
     copied out at the end of its own block (the default defers it behind the
     next block's transpose)."""
