@@ -69,8 +69,8 @@ __device__ __forceinline__ void wave_copy(const lds8* S, int sp, lds8* Dd, int d
     }
     const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
     const int head = q0 - dp, tailn = dp + n - q1;
-    const int e = lane < 4 ? lane : n - tailn + (lane - 4);
-    const bool edge = lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn);
+    const int e = lane + (lane < 4 ? 0 : n - tailn - 4);
+    const bool edge = (lane < head) | ((lane >= 4) & (lane < 4 + tailn));
     const uint32_t eb = edge ? (uint32_t)S[sp + e] : 0u;
     const int nw = (q1 - q0) >> 2;
     for (int c = lane; c < nw; c += kWave) {

@@ -69,6 +69,7 @@ struct IdxArgs {
     int64_t W;           // candidate window (largest record)
     uint32_t maxlen;
     int64_t win_lds;     // k_idx_exits' LDS window bytes
+    int64_t wsub;        // candidates per k_idx_exits workgroup (gridDim.y of them per chunk)
 };
 
 struct ChunkLoc {
@@ -105,7 +106,8 @@ __device__ __forceinline__ ChunkLoc chunk_loc(const IdxArgs& x, int64_t c) {
     return l;
 }
 
-__global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict__ exits) {
+__global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict__ exits,
+                                                  int64_t* __restrict__ his) {
     // the candidate window (largest record + 4, +64 slack), sized at launch:
     // the chases below are latency-bound, so a small window buys residency
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
@@ -118,17 +120,22 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
     const int64_t s = L.s;
     const int64_t cs = s * CH;
     const int64_t ce = min(cs + CH, Cb);
-    const int64_t cend = (s == 0) ? cs + 1 : min(cs + W, Cb);  // candidate window
-    const int64_t wbytes = min(cend + 3, Cb) - cs;
+    // candidate window [cs, cs + W), split over gridDim.y workgroups of wsub
+    // candidates each (large blocks: a window of the largest record does not
+    // fit the LDS, and one wave per chunk would leave most CUs idle)
+    const int64_t cwin = (s == 0) ? cs + 1 : min(cs + W, Cb);
+    const int64_t cb0 = min(cs + (int64_t)blockIdx.y * x.wsub, cwin);
+    const int64_t cend = min(cb0 + x.wsub, cwin);
+    const int64_t wbytes = max(min(cend + 3, Cb) - cb0, (int64_t)0);
     // 16-byte loads of the candidate window, aligned on the ABSOLUTE address:
     // an aligned granule never crosses a page, so the bytes it reads outside
-    // [cs, cs+wbytes) cannot fault and are never used
-    const uintptr_t start = (uintptr_t)(in + cs);
+    // [cb0, cb0+wbytes) cannot fault and are never used
+    const uintptr_t start = (uintptr_t)(in + cb0);
     const int sh = (int)(start & 15);
     const int64_t nch = (sh + wbytes + 15) >> 4;
     const bool use_lds = nch * 16 <= x.win_lds;
     if (use_lds) {
-        const gbl128c* g4 = g128_aligned_down(in + cs);
+        const gbl128c* g4 = g128_aligned_down(in + cb0);
         lds128* w4 = (lds128*)to_lds(win);
         for (int c = lane; c < (int)nch; c += kWave) w4[c] = g4[c];
         __syncthreads();
@@ -147,8 +154,8 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
         // 4 consecutive candidates per lane: two dword reads cover the 7
         // bytes of their four big-endian length words
         const lds8* wq = (const lds8*)to_lds(win) + win_off;
-        for (int64_t c0 = cs + 4 * lane; c0 < cend; c0 += 4 * kWave) {
-            const int r = (int)(c0 - cs);
+        for (int64_t c0 = cb0 + 4 * lane; c0 < cend; c0 += 4 * kWave) {
+            const int r = (int)(c0 - cb0);
             const uint32_t a = lds_rd32(wq, r), b = lds_rd32(wq, r + 4);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -162,7 +169,7 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
         // aligned dword never crosses a page; bytes past Cb are never used),
         // several iterations' loads in flight at once
 #pragma unroll 8
-        for (int64_t c0 = cs + 4 * lane; c0 < cend; c0 += 4 * kWave) {
+        for (int64_t c0 = cb0 + 4 * lane; c0 < cend; c0 += 4 * kWave) {
             const uintptr_t ap = (uintptr_t)(in + c0), al = ap & ~(uintptr_t)3;
             const uint32_t sh = (uint32_t)(ap & 3);
             const uint32_t w0 = *(const gbl32c*)al, w1 = *(const gbl32c*)(al + 4),
@@ -179,7 +186,26 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
         lo = min(lo, (int64_t)__shfl_xor(lo, o));
         hi = max(hi, (int64_t)__shfl_xor(hi, o));
     }
-    if (lane == 0) exits[blockIdx.x] = (hi < 0) ? kDead : (lo == hi ? lo : kAmbiguous);
+    if (gridDim.y == 1) {
+        if (lane == 0) exits[blockIdx.x] = (hi < 0) ? kDead : (lo == hi ? lo : kAmbiguous);
+    } else if (lane == 0) {
+        // split window: min / max of the surviving exits over the chunk's
+        // workgroups (exits[] pre-filled with INT64_MAX, his[] with -1), made
+        // an exit by k_idx_exits_join
+        if (hi >= 0) {
+            atomicMin((long long*)&exits[blockIdx.x], (long long)lo);
+            atomicMax((long long*)&his[blockIdx.x], (long long)hi);
+        }
+    }
+}
+
+// Split windows: one exit per chunk from the min / max the workgroups left.
+__global__ void k_idx_exits_join(int64_t* __restrict__ exits, const int64_t* __restrict__ his,
+                                 int64_t nch) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nch) return;
+    const int64_t lo = exits[c], hi = his[c];
+    exits[c] = (hi < 0) ? kDead : (lo == hi ? lo : kAmbiguous);
 }
 
 // Entry e_s of chunk s (of the stream whose chunk 0 is exits[0]): the agreed
@@ -292,7 +318,9 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
         return;
     }
     const int s = mop - off;
-    const float rinv = 1.0f / (float)off;
+    // v_rcp_f32 (1 ulp): small_mod's one correction step either way and the
+    // [2^16/off, 2^16/off + 2) window below both absorb its error (x < 2^17)
+    const float rinv = __builtin_amdgcn_rcpf((float)off);
     if (ml <= kWave) {
         // i mod off for i < 64, off < 64: q = (i * inv) >> 16 with inv in
         // [2^16 / off, 2^16 / off + 2) is exact (its error i * 2 / 2^16 < 1/512
@@ -322,8 +350,8 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
         const int head = q0 - mop, tailn = mop + ml - q1;
         const uint32_t rot = 8u * (uint32_t)(head & (off - 1));
         const uint32_t w = rot ? (v >> rot) | (v << (32u - rot)) : v;
-        const int e = lane < 4 ? lane : ml - tailn + (lane - 4);
-        if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn))
+        const int e = lane + (lane < 4 ? 0 : ml - tailn - 4);
+        if ((lane < head) | ((lane >= 4) & (lane < 4 + tailn)))
             D[mop + e] = (uint8_t)(v >> (8 * (e & (off - 1))));
         const int nw = (q1 - q0) >> 2;
         lds32* W = (lds32*)(D + q0);
@@ -332,8 +360,8 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
     }
     // <= 3 head and <= 3 tail bytes, then the aligned interior dwords
     const int head = q0 - mop, tailn = mop + ml - q1;
-    const int e = lane < 4 ? lane : ml - tailn + (lane - 4);
-    if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn))
+    const int e = lane + (lane < 4 ? 0 : ml - tailn - 4);
+    if ((lane < head) | ((lane >= 4) & (lane < 4 + tailn)))
         D[mop + e] = D[s + small_mod(e, off, rinv)];
     const int nw = (q1 - q0) >> 2;
     const int step = small_mod(4 * kWave, off, rinv);
@@ -396,8 +424,8 @@ struct GblRec {
         }
         const int q0 = (dp + 3) & ~3, q1 = (dp + n) & ~3;
         const int head = q0 - dp, tailn = dp + n - q1;
-        const int e = lane < 4 ? lane : n - tailn + (lane - 4);
-        if (lane < 4 ? lane < head : (lane < 8 && lane - 4 < tailn)) D[dp + e] = S[e];
+        const int e = lane + (lane < 4 ? 0 : n - tailn - 4);
+        if ((lane < head) | ((lane >= 4) & (lane < 4 + tailn))) D[dp + e] = S[e];
         const int nw = (q1 - q0) >> 2;
         const uintptr_t a0 = base + (uintptr_t)(sp + head);
         const uint32_t sh = (uint32_t)(a0 & 3);
@@ -1315,6 +1343,12 @@ int64_t idx_win_lds(uint32_t maxlen) {
     const int64_t w = ((4 + (int64_t)maxlen + 3 + 16 + 64) + 15) & ~(int64_t)15;
     return w < kIdxWinMax ? w : kIdxWinMax;
 }
+// Candidates per k_idx_exits workgroup: the whole window when it fits the LDS
+// budget, else slices that do (staged in LDS like a small window).
+int64_t idx_wsub(uint32_t maxlen) {
+    const int64_t W = 4 + (int64_t)maxlen;
+    return idx_win_lds(maxlen) < kIdxWinMax ? W : kIdxWinMax - 128;
+}
 
 // Index rebuild over nch chunks (of one stream, or of every stream of a batch).
 hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, const DecodeBufs& b,
@@ -1333,7 +1367,18 @@ hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, cons
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch), dim3(kWave), lds, s, x, b.exits);
+        const int64_t ny = (x.W + x.wsub - 1) / x.wsub;
+        if (ny > 1) {
+            // b.cnt (the walk's counts, written later) holds the maxima meanwhile
+            e = dev_fill(b.exits, 0x7F, (size_t)nch * sizeof(int64_t), s);
+            if (e == hipSuccess) e = dev_fill(b.cnt, 0xFF, (size_t)nch * sizeof(int64_t), s);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_idx_exits, dim3((unsigned)nch, (unsigned)ny), dim3(kWave), lds, s, x, b.exits,
+                           (int64_t*)b.cnt);
+        if (ny > 1)
+            hipLaunchKernelGGL(k_idx_exits_join, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, b.exits,
+                               (const int64_t*)b.cnt, nch);
     }
     const unsigned wg = (unsigned)((nch + 63) / 64);
     {
@@ -1365,7 +1410,7 @@ hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const De
                         hipStream_t s) {
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     IdxArgs x{in, Cb, L.nblocks(), b.idx_err, nullptr, nullptr, nullptr, b.chunk,
-              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen)};
+              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen), idx_wsub(maxlen)};
     return index_impl(x, L.nblocks(), b.nchunks, 1, b, s);
 }
 
@@ -1373,7 +1418,7 @@ hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_
                               int64_t nchunks, const DecodeBufs& b, hipStream_t s) {
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     IdxArgs x{nullptr, 0, L.nfull, nullptr, segs, chunk_seg, b.idx_err, b.chunk,
-              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen)};
+              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen), idx_wsub(maxlen)};
     return index_impl(x, L.nfull, nchunks, nsegs, b, s);
 }
 
