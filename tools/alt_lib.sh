@@ -5,7 +5,7 @@
 set -e
 TAG=$1; shift
 cd "$(dirname "$0")/../bitshuffle_amd"
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I../include -Wno-unused-result -munsafe-fp-atomics -mllvm -structurizecfg-skip-uniform-regions"
+F="--offload-arch=gfx950 ${OPT:--O3} -std=c++17 -fPIC -Wall -I../include -Wno-unused-result -munsafe-fp-atomics -mllvm -structurizecfg-skip-uniform-regions"
 mkdir -p /tmp/alt_$TAG
 /opt/rocm/bin/hipcc $F "$@" -c csrc/lz4_encode.hip -o /tmp/alt_$TAG/lz4_encode.o &
 /opt/rocm/bin/hipcc $F "$@" -c csrc/lz4_decode.hip -o /tmp/alt_$TAG/lz4_decode.o &
