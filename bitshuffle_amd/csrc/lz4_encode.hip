@@ -251,10 +251,12 @@ struct EmitDesc {
     int lane;
     int ns = 0;   // sequences recorded
     int la = 0;   // anchor of the last literal run
+    // Never fails inside the parse (no early exit on its chains): past the
+    // last slot it keeps overwriting that slot, and the caller re-parses the
+    // block with the inline emitter when ns ends above kDescMax.
     __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
-        if (ns >= kDescMax) return false;
-        ((lds64v*)desc)[ns] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
-                                    (uint32_t)(ip - anchor) | ((uint32_t)mc << 16)};
+        ((lds64v*)desc)[min(ns, kDescMax - 1)] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
+                                                      (uint32_t)(ip - anchor) | ((uint32_t)mc << 16)};
         ns++;
         (void)op;
         return true;
@@ -687,7 +689,7 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 ip += mc + kMinMatch;
                 anchor = ip;
                 STAMP(3);
-                if (ip >= limit) break;
+                if (ip >= limit) goto last_literals;  // straight out: the miss exit below stays the only break
                 // fill table at ip-2, then test ip (lz4/lz4.c:1230-1293)
                 const int t = ip - co.tail_base;
                 uint32_t x2, x0, h2, h0;
@@ -770,11 +772,12 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 STAMP(4);
                 break;
             }
-            if (anchor >= limit) break;
+            // a miss: anchor < limit (the re-test ran), search from anchor + 1
             ip = anchor + 1;
         }
     }
     // ---------------------------------------------------- last literals
+last_literals:
     em.last(op, anchor, n);
     STAMP(5);
     COUNT(4, 1);
@@ -1071,6 +1074,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                 EmitDesc em{(lds32*)(D + a.desc_off), lane};
                 c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048))>(D, n, T, em, lane);
                 KSTAMP(1);
+                if (em.ns > kDescMax) c = -1;  // more sequences than descriptor slots
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
