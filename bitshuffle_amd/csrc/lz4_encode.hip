@@ -542,11 +542,11 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                             mpos = __builtin_amdgcn_readlane(pos, js);
                             if (lane > js && cand <= (uint32_t)mpos) T.put(h, cand);
                             mref = __builtin_amdgcn_readlane((int)cand, js);
-                            break;
+                            goto have_match;  // every exit goes straight to its code
                         }
                         seq_cur = seq_nxt;
                     }
-                    if (mpos < 0) {
+                    {
                         // the partial window (if any probe of it is valid)
                         q1 = probe_lane(k0 + lane + 1);
                         const int pos = p0 + q0.off - bias;
@@ -563,8 +563,10 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                                 mpos = __builtin_amdgcn_readlane(pos, js);
                                 if (valid && lane > js && cand <= (uint32_t)mpos) T.put(h, cand);
                                 mref = __builtin_amdgcn_readlane((int)cand, js);
+                                goto have_match;
                             }
                         }
+                        goto last_literals;
                     }
                 }
                 for (int k0 = 0; READBACK || WIDE || (OPT & 512) != 0; k0 += kWave) {
@@ -675,6 +677,7 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
             }
             STAMP(0);
             if (mpos < 0) break;
+        have_match:
             COUNT(0, 1);
             // ------------------------------------------------ catch up + count
             CountOut co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
