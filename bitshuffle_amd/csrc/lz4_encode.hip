@@ -239,6 +239,8 @@ constexpr int kWinBytes = 4 * kWave;  // bytes one dword-per-lane wave access co
 //    descriptor slots, and the A/B variant 2).
 // ---------------------------------------------------------------------------
 
+constexpr int kLaneRun = 128;              // emission: longest literal run copied per lane
+constexpr int kLaneRunMin = 4;             // ... when the batch has at least this many long runs
 constexpr int kDescMax = 256;              // descriptor slots per block
 constexpr int kDescBytes = 8 * kDescMax;   // LDS behind the block
 
@@ -356,8 +358,18 @@ __device__ __forceinline__ int emit_sequences(const lds8* D, const EmitDesc& em,
         if (act) S[op] = (uint8_t)((min(lit, 15) << 4) | (m ? min(mc, 15) : 0));
         lane_len_run(S, op + 1, le, (uint32_t)(lit - 15) % 255u);
         const int lp = op + 1 + le, lsrc = ip - lit;
-        if (lit > 0 && lit <= 16) lane_copy16(D, lsrc, S, lp, lit);
-        for (uint64_t lm = ballot(lit > 16); lm; lm &= lm - 1) {
+        // With several long runs in the batch (literal-heavy data): runs of up
+        // to kLaneRun bytes are copied by their own lanes in 16-byte pieces,
+        // all at once (pieces of neighbouring runs that share a dword land by
+        // masked writes); otherwise, and for longer runs, run by run by the wave
+        const int lane_max =
+            __builtin_popcountll(ballot(lit > 16)) >= kLaneRunMin ? kLaneRun : 16;
+        {
+            const bool mine = lit > 0 && lit <= lane_max;
+            for (int d0 = 0; ballot(mine && d0 < lit) != 0; d0 += 16)
+                if (mine && d0 < lit) lane_copy16(D, lsrc + d0, S, lp + d0, min(16, lit - d0));
+        }
+        for (uint64_t lm = ballot(lit > lane_max); lm; lm &= lm - 1) {
             const int l = ffs64(lm);
             wave_copy(D, __builtin_amdgcn_readlane(lsrc, l), S, __builtin_amdgcn_readlane(lp, l),
                       __builtin_amdgcn_readlane(lit, l), lane);
