@@ -65,6 +65,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="skip per-kernel event timing")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group (RCCL on a GPU) and run the barrier / "
+                         "MAX / SUM collectives even at world size 1 (tests the N>1 code path)")
     return ap.parse_args(argv)
 
 
@@ -94,7 +97,7 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -105,14 +108,27 @@ def dist_setup(args):
     return world, rank, local
 
 
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def dist_info():
+    if not _dist_on():
+        return None
+    import torch.distributed as dist
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "collectives": "barrier + all_reduce MAX/SUM on device tensors"}
+
+
 def barrier(world):
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.barrier()
 
 
 def reduce_over_ranks(x, world, device, op):
-    if world == 1:
+    if not _dist_on():
         return x
     import torch
     import torch.distributed as dist
@@ -123,12 +139,12 @@ def reduce_over_ranks(x, world, device, op):
 
 def max_over_ranks(x, world, device):
     import torch.distributed as dist
-    return reduce_over_ranks(x, world, device, dist.ReduceOp.MAX) if world > 1 else x
+    return reduce_over_ranks(x, world, device, dist.ReduceOp.MAX)
 
 
 def sum_over_ranks(x, world, device):
     import torch.distributed as dist
-    return reduce_over_ranks(x, world, device, dist.ReduceOp.SUM) if world > 1 else x
+    return reduce_over_ranks(x, world, device, dist.ReduceOp.SUM)
 
 
 def timed_loop(step, steps, warmup, world, sync, device):
@@ -582,10 +598,10 @@ def main(argv=None):
                        "ratio": round(nbytes / C, 4) if C else None,
                        "parallelism": "shard-per-gpu x%d" % world},
             "roofline": roofline, "round_trip": stage, "kernels_avg_ms": kernels,
-            "parity": parity, "cpu_baseline": cpu,
+            "parity": parity, "cpu_baseline": cpu, "dist": dist_info(),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 

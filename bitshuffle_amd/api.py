@@ -147,13 +147,27 @@ def decompress_lz4_workspace(in_nbytes, numel, elem_size, block_size=0, device=N
     return torch.empty(max(n, 256), dtype=torch.uint8, device=device or "cuda")
 
 
+def _elems(t, elem_size):
+    """(element count, element size) of tensor t; elem_size overrides the
+    dtype's, for element sizes torch has no dtype for (t is then raw bytes)."""
+    if elem_size is None:
+        return t.numel(), t.element_size()
+    nbytes = t.numel() * t.element_size()
+    if elem_size <= 0 or nbytes % elem_size:
+        raise ValueError("tensor of %d bytes is not a whole number of %d-byte elements"
+                         % (nbytes, elem_size))
+    return nbytes // elem_size, int(elem_size)
+
+
 def compress_lz4_dev(t, block_size=0, out=None, workspace=None, result=None, offsets=None,
-                     stream=None, sync=True):
+                     stream=None, sync=True, elem_size=None):
     """Device-resident bshuf_compress_lz4.  Returns the framed stream as a uint8
     tensor view (sync=True), or (out, result) where result is a 1-element int64
-    device tensor holding the byte count / error (sync=False)."""
+    device tensor holding the byte count / error (sync=False).  `elem_size`
+    overrides the tensor's element size (any E, e.g. a uint8 tensor of
+    7-byte records)."""
     torch = _torch()
-    n, es = t.numel(), t.element_size()
+    n, es = _elems(t, elem_size)
     bound = compress_lz4_bound(n, es, block_size)
     if bound > (1 << 62):
         _fail(-81)
@@ -175,22 +189,27 @@ def compress_lz4_dev(t, block_size=0, out=None, workspace=None, result=None, off
 
 
 def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None, result=None,
-                       offsets=None, stream=None, sync=True):
+                       offsets=None, stream=None, sync=True, elem_size=None):
     """Device-resident bshuf_decompress_lz4 of the whole uint8 tensor `buf`
-    (its length is the exact stream length)."""
+    (its length is the exact stream length).  With `elem_size`, `shape` counts
+    elem_size-byte elements and the output is a uint8 tensor of their bytes."""
     torch = _torch()
     size = 1
     for s in shape:
         size *= int(s)
     if out is None:
-        out = torch.empty(tuple(shape), dtype=dtype, device=buf.device)
+        if elem_size is None:
+            out = torch.empty(tuple(shape), dtype=dtype, device=buf.device)
+        else:
+            out = torch.empty(size * int(elem_size), dtype=torch.uint8, device=buf.device)
+    es = out.element_size() if elem_size is None else int(elem_size)
     if result is None:
         result = torch.empty(1, dtype=torch.int64, device=buf.device)
     ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
     wsb = workspace.numel() if workspace is not None else 0
     offp = _dptr(offsets) if offsets is not None else None
     _check(lib.bshuf_decompress_lz4_dev(_dptr(buf), buf.numel(), _dptr(out), size,
-                                        out.element_size(), block_size, ws, wsb, _dptr(result),
+                                        es, block_size, ws, wsb, _dptr(result),
                                         offp, _stream(stream)))
     if not sync:
         return out, result
@@ -214,21 +233,22 @@ def _size_array(vals):
 
 
 def compress_lz4_batch_dev(tensors, block_size=0, outs=None, workspace=None, offsets=None,
-                           stream=None, sync=True):
+                           stream=None, sync=True, elem_size=None):
     """bshuf_compress_lz4_batch_dev over a list of device tensors (same dtype):
     one launch per kernel for all of them.  Returns the list of framed uint8
     streams (sync=True), or (outs, results) with results a device int64 tensor
-    of per-stream byte counts / error codes."""
+    of per-stream byte counts / error codes.  `elem_size` overrides the
+    tensors' element size (as in compress_lz4_dev)."""
     torch = _torch()
     if not tensors:
         return []
-    es = tensors[0].element_size()
-    sizes = [t.numel() for t in tensors]
+    es = _elems(tensors[0], elem_size)[1]
+    sizes = [_elems(t, elem_size)[0] for t in tensors]
     if outs is None:
         outs = [torch.empty(max(compress_lz4_bound(n, es, block_size), 1), dtype=torch.uint8,
                             device=t.device) for n, t in zip(sizes, tensors)]
     for t in tensors:
-        if t.element_size() != es:
+        if _elems(t, elem_size)[1] != es:
             raise ValueError("all tensors of a batch need the same element size")
         _dptr(t)
     results = torch.empty(len(tensors), dtype=torch.int64, device=tensors[0].device)
@@ -250,17 +270,33 @@ def compress_lz4_batch_dev(tensors, block_size=0, outs=None, workspace=None, off
 
 
 def decompress_lz4_batch_dev(bufs, shapes, dtype, block_size=0, outs=None, workspace=None,
-                             stream=None, sync=True):
+                             stream=None, sync=True, elem_size=None):
     """bshuf_decompress_lz4_batch_dev: each uint8 device tensor of `bufs` is one
     whole framed stream; returns the decoded tensors (sync=True), or (outs,
-    results) with per-stream consumed byte counts / error codes."""
+    results) with per-stream consumed byte counts / error codes.  With
+    `elem_size`, shapes count elem_size-byte elements and the outputs are
+    uint8 tensors of their bytes."""
     torch = _torch()
     if not bufs:
         return []
+
+    def count(sh):
+        c = 1
+        for x in sh:
+            c *= int(x)
+        return c
     if outs is None:
-        outs = [torch.empty(tuple(sh), dtype=dtype, device=b.device) for b, sh in zip(bufs, shapes)]
-    es = outs[0].element_size()
-    sizes = [o.numel() for o in outs]
+        if elem_size is None:
+            outs = [torch.empty(tuple(sh), dtype=dtype, device=b.device) for b, sh in zip(bufs, shapes)]
+        else:
+            outs = [torch.empty(count(sh) * int(elem_size), dtype=torch.uint8, device=b.device)
+                    for b, sh in zip(bufs, shapes)]
+    if elem_size is None:
+        es = outs[0].element_size()
+        sizes = [o.numel() for o in outs]
+    else:
+        es = int(elem_size)
+        sizes = [count(sh) for sh in shapes]
     nbytes = [b.numel() for b in bufs]
     results = torch.empty(len(bufs), dtype=torch.int64, device=bufs[0].device)
     pin, keep1 = _ptr_array([_dptr(b).value or 0 for b in bufs])

@@ -185,7 +185,7 @@ struct HostCtx {
     uint32_t* flags_host = nullptr;  // 2 x kXferMaxGrid words
     uint32_t* flags_dev = nullptr;
     int next = 0;
-    bool broken = false;  // a transport wait failed: refuse further work
+    bool broken = false;  // a transport wait failed: these buffers are abandoned
 
     ~HostCtx() {
         if (!s) return;
@@ -199,6 +199,19 @@ struct HostCtx {
         }
         if (flags_host) (void)hipHostFree(flags_host);
         (void)hipStreamDestroy(s);
+    }
+
+    // forget every handle without releasing it (see host_ctx)
+    void abandon() {
+        s = nullptr;
+        for (int i = 0; i < kN; i++) {
+            buf[i] = nullptr;
+            cap[i] = 0;
+        }
+        for (Slot& x : slot) x = Slot{};
+        flags_host = flags_dev = nullptr;
+        next = 0;
+        broken = false;
     }
 
     bool init() {
@@ -294,8 +307,14 @@ struct HostCtx {
 
 thread_local HostCtx t_ctx;
 
+// After a failed transfer the thread's stream, device buffers and pinned
+// slots are abandoned (a lost transfer may still land in them later: they are
+// never reused, and leaked rather than freed under it) and the next call
+// starts over with fresh ones -- one transient fault does not disable the
+// thread's later calls.
 HostCtx* host_ctx() {
-    if (t_ctx.broken || !t_ctx.init()) return nullptr;
+    if (t_ctx.broken) t_ctx.abandon();
+    if (!t_ctx.init()) return nullptr;
     return &t_ctx;
 }
 
@@ -440,38 +459,89 @@ int64_t transpose_host(const void* in, void* out, size_t size, size_t elem_size,
     return n;
 }
 
-// Per-thread pinned buffer of stage_upload (the batch segment tables).
-struct TableStage {
+// Per-thread pinned buffers of stage_upload (the batch segment tables), as a
+// ring: a buffer is reused only once the upload kernel that read it has stored
+// its flag word, so a batch call never waits for an earlier call's kernel while
+// a free buffer exists (bitshuffle.h: nothing synchronises the host).  With
+// kTableRing uploads still queued, the oldest one's event is waited on -- with
+// no time limit, however much work is queued in front of it.  Under stream
+// capture a buffer is never reused (the captured kernel reads it at every
+// replay of the graph): it is kept for the life of the process.
+constexpr int kTableRing = 16;
+struct TableBuf {
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
-    uint32_t* flags_host = nullptr;
-    uint32_t* flags_dev = nullptr;
+    hipEvent_t ev = nullptr;
     uint32_t seq = 0;
-    int nwg = 0;
+    bool busy = false;
+};
+struct TableStage {
+    TableBuf buf[kTableRing];
+    int nbuf = 0;
+    int oldest = 0;                   // the next buffer to wait for when all are busy
+    uint32_t* flags_host = nullptr;   // one word per ring buffer
+    uint32_t* flags_dev = nullptr;
     ~TableStage() {
-        if (host) (void)hipHostFree(host);
+        for (int i = 0; i < nbuf; i++) {
+            if (buf[i].busy && buf[i].ev) (void)hipEventSynchronize(buf[i].ev);
+            if (buf[i].host) (void)hipHostFree(buf[i].host);
+            if (buf[i].ev) (void)hipEventDestroy(buf[i].ev);
+        }
         if (flags_host) (void)hipHostFree(flags_host);
     }
-    // the previous upload's kernel has read the buffer (its flags are set)
-    bool settle() {
-        if (!nwg) return true;
-        volatile uint32_t* f = flags_host;
-        const time_t t0 = time(nullptr);
-        for (int w = 0; w < nwg;) {
-            if (f[w] == seq) {
-                w++;
-                continue;
+    bool done(int i) const {
+        const TableBuf& b = buf[i];
+        return !b.busy || ((volatile const uint32_t*)flags_host)[i] == b.seq;
+    }
+    // a buffer whose previous upload has been read (-1: none could be made)
+    int acquire() {
+        for (int i = 0; i < nbuf; i++)
+            if (done(i)) {
+                std::atomic_thread_fence(std::memory_order_acquire);
+                buf[i].busy = false;
+                return i;
             }
-            if (time(nullptr) - t0 > 30) return false;
+        if (nbuf < kTableRing) {
+            if (hipEventCreateWithFlags(&buf[nbuf].ev, hipEventDisableTiming) != hipSuccess) return -1;
+            return nbuf++;
+        }
+        const int i = oldest;
+        oldest = (oldest + 1) % kTableRing;
+        if (hipEventSynchronize(buf[i].ev) != hipSuccess) return -1;
+        // the kernel has completed: its flag store is visible (bounded wait
+        // only as a guard against a transport fault)
+        const time_t t0 = time(nullptr);
+        while (!done(i)) {
+            if (time(nullptr) - t0 > 30) return -1;
             sched_yield();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
-        nwg = 0;
-        return true;
+        buf[i].busy = false;
+        return i;
     }
 };
 thread_local TableStage t_table;
+
+// The flag word of captured uploads (written at every replay, never read).
+uint32_t* t_captured_flags() {
+    static uint32_t* dev = nullptr;
+    static std::atomic<bool> made{false};
+    static std::atomic_flag lock = ATOMIC_FLAG_INIT;
+    if (made.load(std::memory_order_acquire)) return dev;
+    while (lock.test_and_set(std::memory_order_acquire)) sched_yield();
+    if (!made.load(std::memory_order_relaxed)) {
+        void* h = nullptr;
+        void* d = nullptr;
+        if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
+            hipHostGetDevicePointer(&d, h, 0) == hipSuccess) {
+            dev = (uint32_t*)d;
+            made.store(true, std::memory_order_release);
+        }
+    }
+    lock.clear(std::memory_order_release);
+    return dev;
+}
 
 }  // namespace
 
@@ -479,35 +549,52 @@ namespace bshuf {
 
 hipError_t stage_upload(const void* host, size_t bytes, void* dev, hipStream_t s) {
     TableStage& t = t_table;
-    if (!t.settle()) return hipErrorUnknown;
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) return hipErrorUnknown;
+    if (cap != hipStreamCaptureStatusNone) {
+        // captured: a buffer of its own, kept for the graph's replays
+        void* h = nullptr;
+        void* d = nullptr;
+        if (hipHostMalloc(&h, bytes + 64, fl) != hipSuccess) return hipErrorOutOfMemory;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return hipErrorUnknown;
+        memcpy(h, host, bytes);
+        XferArgs a{(uint8_t*)dev, (const uint8_t*)d, (int64_t)bytes, t_captured_flags(), 1};
+        if (!a.flags) return hipErrorOutOfMemory;
+        hipLaunchKernelGGL(k_xfer<false>, dim3(1), dim3(kXferThreads), 0, s, a);
+        return hipGetLastError();
+    }
     if (!t.flags_host) {
         void* f = nullptr;
-        if (hipHostMalloc(&f, kXferMaxGrid * sizeof(uint32_t), fl) != hipSuccess) return hipErrorOutOfMemory;
+        if (hipHostMalloc(&f, kTableRing * sizeof(uint32_t), fl) != hipSuccess) return hipErrorOutOfMemory;
         t.flags_host = (uint32_t*)f;
-        memset(f, 0, kXferMaxGrid * sizeof(uint32_t));
+        memset(f, 0, kTableRing * sizeof(uint32_t));
         void* fd = nullptr;
         if (hipHostGetDevicePointer(&fd, f, 0) != hipSuccess) return hipErrorUnknown;
         t.flags_dev = (uint32_t*)fd;
     }
-    if (t.cap < bytes) {
-        if (t.host) (void)hipHostFree(t.host);
-        t.host = t.dev = nullptr;
-        t.cap = 0;
+    const int i = t.acquire();
+    if (i < 0) return hipErrorUnknown;
+    TableBuf& b = t.buf[i];
+    if (b.cap < bytes) {
+        if (b.host) (void)hipHostFree(b.host);
+        b.host = b.dev = nullptr;
+        b.cap = 0;
         void* h = nullptr;
         if (hipHostMalloc(&h, bytes + 64, fl) != hipSuccess) return hipErrorOutOfMemory;
         void* d = nullptr;
         if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return hipErrorUnknown;
-        t.host = (uint8_t*)h;
-        t.dev = (uint8_t*)d;
-        t.cap = bytes;
+        b.host = (uint8_t*)h;
+        b.dev = (uint8_t*)d;
+        b.cap = bytes;
     }
-    memcpy(t.host, host, bytes);
-    t.seq = t.seq + 1 == 0 ? 1 : t.seq + 1;
-    XferArgs a{(uint8_t*)dev, t.dev, (int64_t)bytes, t.flags_dev, t.seq};
+    memcpy(b.host, host, bytes);
+    b.seq = b.seq + 1 == 0 ? 1 : b.seq + 1;
+    XferArgs a{(uint8_t*)dev, b.dev, (int64_t)bytes, t.flags_dev + i, b.seq};
     hipLaunchKernelGGL(k_xfer<false>, dim3(1), dim3(kXferThreads), 0, s, a);
-    const hipError_t e = hipGetLastError();
-    if (e == hipSuccess) t.nwg = 1;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(b.ev, s);
+    if (e == hipSuccess) b.busy = true;
     return e;
 }
 
@@ -669,8 +756,17 @@ int64_t host_step(const void* in, void* out, size_t size, size_t elem_size, Op o
     return (int64_t)bytes;
 }
 
+// The one-block hooks run the whole array as ONE bitshuffle block: up to
+// kMaxOneBlock bytes and elem_size <= 65536 (make_plan's device limits),
+// checked before anything touches the device (bitshuffle_internals.h).
+constexpr size_t kMaxOneBlock = (size_t)INT32_MAX / 2;
+bool one_block_ok(size_t size, size_t elem_size) {
+    return elem_size <= 65536 && (elem_size == 0 || size <= kMaxOneBlock / elem_size);
+}
+
 int64_t bit_block(const void* in, void* out, size_t size, size_t elem_size, bool fwd) {
     if (size % 8) return kErrNotMult8;
+    if (!one_block_ok(size, elem_size)) return kErrUnsupported;
     return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
         return fwd ? bshuf_bitshuffle_dev(di, dout, size, elem_size, size, s)
                    : bshuf_bitunshuffle_dev(di, dout, size, elem_size, size, s);
@@ -702,6 +798,7 @@ int64_t bshuf_trans_byte_elem_scal(const void* in, void* out, const size_t size,
 int64_t bshuf_trans_bit_byte_scal(const void* in, void* out, const size_t size, const size_t elem_size) {
     const size_t nbyte = size * elem_size;
     if (nbyte % 8) return kErrNotMult8;
+    if (!one_block_ok(nbyte, 1)) return kErrUnsupported;
     return host_step(in, out, size, elem_size, [&](uint8_t* di, uint8_t* dout, hipStream_t s) {
         return bshuf_bitshuffle_dev(di, dout, nbyte, 1, nbyte, s);
     });

@@ -19,6 +19,12 @@
  *
  * Host pointers, sizes in ELEMENTS, return size*elem_size or a negative code
  * (-80: a size that must be a multiple of 8 is not; -70: no HIP device).
+ * Limit (a deviation: the reference's scalar functions have none): the
+ * one-block bit transposes -- bshuf_trans_bit_byte_scal, bshuf_trans_bit_elem
+ * (_scal), bshuf_untrans_bit_elem(_scal) -- run the whole array as ONE
+ * bitshuffle block, so size*elem_size must stay below 2^30 bytes and
+ * elem_size at most 65536; larger calls return -71 before touching the
+ * device.
  * The scalar and ISA-dispatched variants run on the GPU (no CPU compute path):
  * the bit transposes are one-block calls of the codec's transpose kernels, the
  * byte-level steps small permutation kernels.  The CPU SIMD variants report

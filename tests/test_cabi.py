@@ -77,3 +77,18 @@ def test_no_cpu_fallback_without_gpu():
         with pytest.raises(RuntimeError) as ei:
             f(np.arange(1024, dtype=np.int16))
         assert ei.value.args[1] == -70
+
+
+def test_one_block_hooks_limit_before_device():
+    """bitshuffle_internals.h: the one-block bit-transpose hooks run the whole
+    array as one block; above 2^30 bytes or elem_size 65536 they return -71
+    before touching any memory (NULL pointers are never dereferenced)."""
+    import bitshuffle_amd as B
+    for name in ("bshuf_trans_bit_elem", "bshuf_trans_bit_elem_scal", "bshuf_untrans_bit_elem",
+                 "bshuf_untrans_bit_elem_scal"):
+        f = getattr(B.lib, name)
+        assert f(None, None, 1 << 31, 1) == -71, name
+        assert f(None, None, (1 << 30) // 4 + 8, 4) == -71, name
+        assert f(None, None, 8, 65537) == -71, name
+        assert f(None, None, 9, 1) == -80, name
+    assert B.lib.bshuf_trans_bit_byte_scal(None, None, 1 << 31, 1) == -71

@@ -547,3 +547,72 @@ def test_large_blocks_match_oracle(bs, oracle, torch, block_bytes):
     dec = bs.decompress_lz4_batch_dev(outs, [x.shape for x in xs], torch.int16, block_bytes // 2)
     for x, d in zip(xs, dec):
         assert torch.equal(x, d)
+
+
+# ------------------------------------------------------------------ reference dtypes
+# The element sizes of the reference's own test matrix (tests/test_ext.py:19-28:
+# S3..S48 and complex128) beyond the ones above, plus E = 64 (the first size
+# whose default block is BSHUF_MIN_RECOMMEND_BLOCK = 128 elements,
+# src/bitshuffle_core.c:2038-2046) and E = 1024, whose DEFAULT block is
+# 128 KiB: byU32 table in the encoder, the large-block decoder.
+REF_E = [7, 9, 11, 16, 48, 64, 1024]
+
+
+def _ref_e_input(E, kind, nblk_default):
+    """A whole number of default blocks, a partial block and a raw tail."""
+    bs_def = max(8192 // E // 8 * 8, 128)
+    n = nblk_default * bs_def + (bs_def // 3) // 8 * 8 + 5
+    rng = np.random.default_rng(1000 * E + len(kind))
+    if kind == "random":  # as the reference's own test data: randint(0, 200)
+        d = rng.integers(0, 200, n * E, dtype=np.uint8)
+    else:  # a slowly varying byte walk: long LZ4 matches after the transpose
+        d = (rng.integers(-2, 3, n * E).cumsum() % 251).astype(np.uint8)
+    return view_e(d, E), n, bs_def
+
+
+@pytest.mark.parametrize("E", REF_E)
+def test_reference_dtypes_transpose(bs, oracle, E):
+    arr, n, bs_def = _ref_e_input(E, "walk", 2)
+    for block in [0, 8, bs_def // 2 // 8 * 8 or 8]:
+        want = oracle.bitshuffle(arr, block)
+        got = bs.bitshuffle(arr, block)
+        assert got.tobytes() == want.tobytes(), (E, block)
+        assert bs.bitunshuffle(got, block).tobytes() == arr.tobytes(), (E, block)
+
+
+@pytest.mark.parametrize("E", REF_E)
+def test_reference_dtypes_lz4_host(bs, oracle, E):
+    """Host C-ABI (bshuf_compress_lz4 / bshuf_decompress_lz4), default and
+    explicit block sizes, random and correlated bytes, vs the oracle."""
+    assert bs.default_block_size(E) == max(8192 // E // 8 * 8, 128)
+    for kind in ("random", "walk"):
+        arr, n, bs_def = _ref_e_input(E, kind, 2)
+        for block in [0, 64, bs_def // 2 // 8 * 8 or 8]:
+            want = oracle.compress_lz4(arr, block)
+            got = bs.compress_lz4(arr, block)
+            assert got.tobytes() == want.tobytes(), (E, kind, block)
+            back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
+            assert back.tobytes() == arr.tobytes(), (E, kind, block)
+
+
+@pytest.mark.parametrize("E", REF_E)
+def test_reference_dtypes_lz4_device_and_batch(bs, oracle, torch, E):
+    """The same element sizes through the device C-ABI (parallel index rebuild
+    on decode) and the batch C-ABI, default block size (block_size = 0) and one
+    explicit block size, vs the oracle."""
+    streams = [_ref_e_input(E, "walk", k)[0] for k in (2, 1)] + [_ref_e_input(E, "random", 1)[0]]
+    for block in (0, 64):
+        wants = [oracle.compress_lz4(a, block) for a in streams]
+        for a, want in zip(streams, wants):
+            t = torch.from_numpy(a.view(np.uint8).copy()).cuda()
+            c = bs.compress_lz4_dev(t, block, elem_size=E)
+            assert c.cpu().numpy().tobytes() == want.tobytes(), (E, block, a.size)
+            d = bs.decompress_lz4_dev(c.clone(), a.shape, None, block, elem_size=E)
+            assert d.cpu().numpy().tobytes() == a.view(np.uint8).tobytes(), (E, block, a.size)
+        xs = [torch.from_numpy(a.view(np.uint8).copy()).cuda() for a in streams]
+        outs = bs.compress_lz4_batch_dev(xs, block, elem_size=E)
+        for o, want in zip(outs, wants):
+            assert o.cpu().numpy().tobytes() == want.tobytes(), (E, block, "batch")
+        dec = bs.decompress_lz4_batch_dev(outs, [a.shape for a in streams], None, block, elem_size=E)
+        for a, d in zip(streams, dec):
+            assert d.cpu().numpy().tobytes() == a.view(np.uint8).tobytes(), (E, block, "batch")
