@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <atomic>
+#include <type_traits>
 #include <cstdlib>
 #include <mutex>
 
@@ -333,7 +334,8 @@ struct EmitBytes {
 // (lane = sequence; a prefix sum places every sequence): record payload at
 // S[4..), literals from the block D.  The last literal run is sequence ns.
 // Returns the payload size.
-__device__ __forceinline__ int emit_sequences(const lds8* D, const EmitDesc& em, const int n, lds8* S,
+template <class Em>
+__device__ __forceinline__ int emit_sequences(const lds8* D, const Em& em, const int n, lds8* S,
                                               const int lane) {
     const int ns = em.ns, la = em.la;
     int opb = 4;
@@ -502,6 +504,305 @@ __device__ __forceinline__ uint32_t win_rd32(uint32_t v, int base, int p) {
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(t & 3));
 }
 
+// ---------------------------------------------------------------------------
+// Descriptors buffered in VGPRs (the hand-scheduled re-test below): sequence
+// s's two descriptor dwords go into lane s % 64 of dlo / dhi by v_writelane
+// (no LDS access on the parse's chain), and every 64 sequences the wave stores
+// the batch with one coalesced ds_write2 into the same LDS slots EmitDesc
+// uses.  Past kDescMax the batches are dropped (the caller re-parses with the
+// inline emitter, as with EmitDesc).
+// ---------------------------------------------------------------------------
+struct EmitDescV {
+    lds32* desc;
+    int lane;
+    int ns = 0;
+    int la = 0;
+    uint32_t dlo = 0, dhi = 0;
+    __device__ __forceinline__ void store_batch(int first, int count) const {
+        if (first < kDescMax && lane < count) ((lds64v*)desc)[first + lane] = u32x2{dlo, dhi};
+    }
+    __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
+        (void)op;
+        const int slot = ns & (kWave - 1);
+        if (lane == slot) {
+            dlo = (uint32_t)ip | ((uint32_t)off << 16);
+            dhi = (uint32_t)(ip - anchor) | ((uint32_t)mc << 16);
+        }
+        ns++;
+        if ((ns & (kWave - 1)) == 0) store_batch(ns - kWave, kWave);
+        return true;
+    }
+    __device__ __forceinline__ void last(int& op, int anchor, int n) {
+        (void)op;
+        (void)n;
+        la = anchor;
+        store_batch(ns & ~(kWave - 1), ns & (kWave - 1));
+    }
+};
+
+// The full search windows of the parse (every probe of the window and its
+// successor inside mflimit, lz4/lz4.c:1042-1075) as one hand-scheduled loop:
+// per window one hash per lane, ONE lane-ordered ds_mskor_rtn exchange, the
+// candidates' bytes, one ballot; the next window's bytes are read beside the
+// exchange.  State: vpos / vseq the current window's probe positions and
+// their bytes, vnxt / vstep the next window's positions and the step after,
+// qs / qstep the next window's lane-0 position (the current last lane's
+// successor) on the scalar unit.  Exits:
+//  kSrPartial  the next window is not full: the caller runs it (nwin full
+//              windows were done);
+//  kSrMatch    lane js of the current window matched; vcand holds every
+//              lane's exchanged-out entry (candidate in its low 16 bits).
+enum { kSrPartial = 0, kSrMatch = 1 };
+
+__device__ __forceinline__ int search_chain(uint32_t& vpos, uint32_t& vnxt, uint32_t& vstep, uint32_t& vseq,
+                                            int& qs, int& qstep, int& nwin, uint32_t& vcand, int& js,
+                                            const int limit, const int n) {
+    int code;
+    uint32_t vh, va, vsh, vad, vm, vd, vold, vlo, vhi, vx1;
+    asm volatile(
+        "L_stop%=:\n\t"
+        "s_cmp_gt_i32 %[qs], %[limit]\n\t"
+        "s_cbranch_scc1 L_spart%=\n\t"
+        "v_mul_lo_u32 %[vh], %[vseq], %[kmul]\n\t"
+        "v_min_i32 %[va], %[n], %[vnxt]\n\t"
+        "s_add_u32 %[qs], %[qs], %[qstep]\n\t"
+        "s_add_u32 %[qstep], %[qstep], 64\n\t"
+        "v_lshrrev_b32 %[vsh], 15, %[vh]\n\t"
+        "v_lshrrev_b32 %[vad], 18, %[vh]\n\t"
+        "v_and_b32 %[vsh], 16, %[vsh]\n\t"
+        "v_and_b32 %[vad], 0x3ffc, %[vad]\n\t"
+        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t"
+        "v_lshlrev_b32 %[vd], %[vsh], %[vpos]\n\t"
+        "v_and_b32 %[vh], -4, %[va]\n\t"
+        "ds_mskor_rtn_b32 %[vold], %[vad], %[vm], %[vd]\n\t"
+        "ds_read_b32 %[vlo], %[vh] offset:16384\n\t"
+        "ds_read_b32 %[vhi], %[vh] offset:16388\n\t"
+        "v_and_b32 %[va], 3, %[va]\n\t"
+        "s_waitcnt lgkmcnt(2)\n\t"
+        "v_lshrrev_b32 %[vcand], %[vsh], %[vold]\n\t"
+        "v_bfe_u32 %[vm], %[vold], %[vsh], 2\n\t"
+        "v_and_b32 %[vd], 0xfffc, %[vcand]\n\t"
+        "ds_read_b32 %[vold], %[vd] offset:16384\n\t"
+        "ds_read_b32 %[vx1], %[vd] offset:16388\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_alignbyte_b32 %[vold], %[vx1], %[vold], %[vm]\n\t"
+        "v_cmp_eq_u32 vcc, %[vold], %[vseq]\n\t"
+        "s_cbranch_vccnz L_smatch%=\n\t"
+        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[va]\n\t"
+        "v_mov_b32 %[vpos], %[vnxt]\n\t"
+        "v_add_u32 %[vnxt], %[vnxt], %[vstep]\n\t"
+        "v_add_u32 %[vstep], 64, %[vstep]\n\t"
+        "s_add_u32 %[nwin], %[nwin], 1\n\t"
+        "s_branch L_stop%=\n\t"
+        "L_smatch%=:\n\t"
+        "s_ff1_i32_b64 %[js], vcc\n\t"
+        "s_mov_b32 %[code], 1\n\t"
+        "s_branch L_send%=\n\t"
+        "L_spart%=:\n\t"
+        "s_mov_b32 %[code], 0\n\t"
+        "L_send%=:"
+        : [code] "=&s"(code), [js] "=&s"(js), [qs] "+s"(qs), [qstep] "+s"(qstep), [nwin] "+s"(nwin),
+          [vpos] "+v"(vpos), [vnxt] "+v"(vnxt), [vstep] "+v"(vstep), [vseq] "+v"(vseq),
+          [vcand] "=&v"(vcand), [vh] "=&v"(vh), [va] "=&v"(va), [vsh] "=&v"(vsh), [vad] "=&v"(vad),
+          [vm] "=&v"(vm), [vd] "=&v"(vd), [vold] "=&v"(vold), [vlo] "=&v"(vlo), [vhi] "=&v"(vhi),
+          [vx1] "=&v"(vx1)
+        : [limit] "s"(limit), [n] "s"(n), [kmul] "s"(2654435761u), [ffff] "s"(0xFFFFu)
+        : "vcc", "scc", "memory");
+    return code;
+}
+
+// The re-test chain of lz4/lz4.c:1230-1293 -- emit the sequence, step past
+// the match, insert ip-2, look up and insert ip, test 4 bytes, count the
+// match -- as ONE hand-scheduled loop: a straight line with one taken branch
+// per zero-literal sequence.
+//  * The bytes at ip-2 and ip come from the previous count window's a-side
+//    registers (`tail`, window start `tb`): a DPP wave shift gives every lane
+//    its neighbour's dword, two v_alignbyte + two v_readlane pick them out;
+//    the hashes run on the scalar unit.
+//  * The table put / get / put are plain LDS ops by every lane (same address,
+//    same value); the count's a-side window is in flight beside them.
+//  * Test and count come from one ballot: lane 0's bit is the 4-byte test,
+//    the first set bit the first differing dword.
+//  * Descriptors go to lane ns % 64 of dlo / dhi (EmitDescV), M0 the lane.
+// Entry: the sequence (ip, ref, mc, lit = ip - anchor) is found and counted.
+// Exits (ip is past the last emitted sequence = the new anchor):
+//  kRtLimit  ip >= mflimitPlusOne: last literals;
+//  kRtMiss   the 4 bytes at ip differ from the table's candidate (table
+//            updated): search from ip + 1;
+//  kRtSlow   ip - 2 or ip + 3 lies outside the register window: the caller
+//            does this re-test (hashes, table, test, count) itself;
+//  kRtLong   table updated, candidate c2, and the first 256 bytes at ip all
+//            equal: the caller counts on.
+// Wait states: every VALU result read by v_readlane / DPP / v_readfirstlane
+// has at least two instructions in between; SALU reads of VALU-written
+// SGPRs / VCC are interlocked.  All LDS reads are waited for inside.
+enum { kRtLimit = 0, kRtMiss = 1, kRtSlow = 2, kRtLong = 3 };
+
+#define BSHUF_RETEST_ASM(P2_BRANCH, P2_BLOCK) \
+    asm volatile( \
+        "s_mov_b32 %[keep], m0\n\t" \
+        "L_top%=:\n\t" \
+        /* ---- sequence descriptor -> lane ns % 64 of dlo / dhi */ \
+        "s_sub_u32 %[t0], %[ip], %[ref]\n\t" \
+        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t" \
+        "s_pack_ll_b32_b16 %[t1], %[lit], %[mc]\n\t" \
+        "s_and_b32 m0, %[ns], 63\n\t" \
+        "s_add_u32 %[ns], %[ns], 1\n\t" \
+        "s_add_u32 %[ip], %[ip], %[mc]\n\t" \
+        "v_writelane_b32 %[dlo], %[t0], m0\n\t" \
+        "v_writelane_b32 %[dhi], %[t1], m0\n\t" \
+        "s_and_b32 %[t2], %[ns], 63\n\t" \
+        "s_cbranch_scc0 L_flush%=\n\t" \
+        "L_flushed%=:\n\t" \
+        /* ---- step past the match; mflimit */ \
+        "s_add_u32 %[ip], %[ip], 4\n\t" \
+        "s_mov_b32 %[lit], 0\n\t" \
+        "s_cmp_ge_i32 %[ip], %[limit]\n\t" \
+        "s_cbranch_scc1 L_lim%=\n\t" \
+        /* ---- ip - 2 .. ip + 3 inside the register window? */ \
+        "s_sub_u32 %[t0], %[ip], %[tb]\n\t" \
+        "s_sub_u32 %[t1], %[t0], 2\n\t" \
+        "s_cmp_gt_u32 %[t1], 249\n\t" \
+        "s_cbranch_scc1 L_slow%=\n\t" \
+        "v_mov_b32_dpp %[vn], %[tail] wave_shl:1 bound_ctrl:0\n\t" \
+        "s_and_b32 %[t2], %[t0], 3\n\t" \
+        "s_and_b32 %[t3], %[t1], 3\n\t" \
+        "s_lshr_b32 %[t0], %[t0], 2\n\t" \
+        "v_alignbyte_b32 %[vy], %[vn], %[tail], %[t2]\n\t" \
+        "v_alignbyte_b32 %[vz], %[vn], %[tail], %[t3]\n\t" \
+        "s_lshr_b32 %[t1], %[t1], 2\n\t" \
+        "s_sub_u32 %[t2], %[ip], 2\n\t" \
+        "v_readlane_b32 %[t0], %[vy], %[t0]\n\t" \
+        "v_readlane_b32 %[t1], %[vz], %[t1]\n\t" \
+        P2_BRANCH \
+        /* ---- hash4 (lz4/lz4.c:762-768) -> entry byte addresses */ \
+        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t" \
+        "s_mul_i32 %[t1], %[t1], 0x9e3779b1\n\t" \
+        "s_lshr_b32 %[t0], %[t0], 18\n\t" \
+        "s_lshr_b32 %[t1], %[t1], 18\n\t" \
+        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t" \
+        "s_and_b32 %[t1], %[t1], 0x3ffe\n\t" \
+        "s_and_b32 %[t3], %[ip], -4\n\t" \
+        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t" \
+        "v_mov_b32 %[vn], %[t1]\n\t" \
+        "v_mov_b32 %[vy], %[t2]\n\t" \
+        "v_mov_b32 %[vz], %[t0]\n\t" \
+        "v_mov_b32 %[vd0], %[ip]\n\t" \
+        /* a-side count window at ip, then put(ip-2), get(ip), put(ip) */ \
+        "ds_read_b32 %[val], %[vcb]\n\t" \
+        "ds_read_b32 %[vah], %[vcb] offset:4\n\t" \
+        "ds_write_b16 %[vn], %[vy]\n\t" \
+        "ds_read_u16 %[vc2], %[vz]\n\t" \
+        "ds_write_b16 %[vz], %[vd0]\n\t" \
+        "s_and_b32 %[t3], %[ip], 3\n\t" \
+        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t" \
+        "s_waitcnt lgkmcnt(1)\n\t" \
+        "v_and_b32 %[vcb], -4, %[vc2]\n\t" \
+        "v_add_u32 %[vcb], %[vcb], %[lane4d]\n\t" \
+        "ds_read_b32 %[vbl], %[vcb]\n\t" \
+        "ds_read_b32 %[vbh], %[vcb] offset:4\n\t" \
+        "v_readfirstlane_b32 %[c2], %[vc2]\n\t" \
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t" \
+        "s_and_b32 %[t2], %[c2], 3\n\t" \
+        "s_waitcnt lgkmcnt(0)\n\t" \
+        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t2]\n\t" \
+        "L_cmp%=:\n\t" \
+        "v_cmp_ne_u32 vcc, %[tail], %[vbl]\n\t" \
+        "v_xor_b32 %[vbh], %[tail], %[vbl]\n\t" \
+        "s_bitcmp1_b32 vcc_lo, 0\n\t" \
+        "s_cbranch_scc1 L_miss%=\n\t" \
+        "s_cmp_eq_u64 vcc, 0\n\t" \
+        "s_cbranch_scc1 L_long%=\n\t" \
+        /* ---- count: first differing byte of the window */ \
+        "s_ff1_i32_b64 %[t0], vcc\n\t" \
+        "s_mov_b32 %[ref], %[c2]\n\t" \
+        "v_readlane_b32 %[t2], %[vbh], %[t0]\n\t" \
+        "s_lshl_b32 %[t0], %[t0], 2\n\t" \
+        "s_mov_b32 %[tb], %[ip]\n\t" \
+        "s_ff1_i32_b32 %[t2], %[t2]\n\t" \
+        "s_lshr_b32 %[t2], %[t2], 3\n\t" \
+        "s_add_u32 %[t0], %[t0], %[t2]\n\t" \
+        "s_min_i32 %[t0], %[t0], %[t1]\n\t" \
+        "s_sub_u32 %[mc], %[t0], 4\n\t" \
+        "s_branch L_top%=\n\t" \
+        /* ---- a batch of 64 descriptors to LDS (dropped past kDescMax) */ \
+        "L_flush%=:\n\t" \
+        "s_sub_u32 %[t2], %[ns], 64\n\t" \
+        "s_cmp_ge_u32 %[t2], 256\n\t" /* kDescMax */ \
+        "s_cbranch_scc1 L_flushed%=\n\t" \
+        "s_lshl_b32 %[t2], %[t2], 3\n\t" \
+        "s_add_u32 %[t2], %[t2], %[desc]\n\t" \
+        "v_add_u32 %[vcb], %[t2], %[lane8]\n\t" \
+        "ds_write2_b32 %[vcb], %[dlo], %[dhi] offset1:1\n\t" \
+        "s_branch L_flushed%=\n\t" \
+        P2_BLOCK \
+        "L_lim%=:\n\t" \
+        "s_mov_b32 %[code], 0\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_miss%=:\n\t" \
+        "s_mov_b32 %[code], 1\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_slow%=:\n\t" \
+        "s_mov_b32 %[code], 2\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_long%=:\n\t" \
+        "s_mov_b32 %[code], 3\n\t" \
+        "L_end%=:\n\t" \
+        "s_mov_b32 m0, %[keep]" \
+        : [code] "=&s"(code), [c2] "=&s"(c2), [ip] "+s"(ip), [ref] "+s"(ref), [mc] "+s"(mc), \
+          [lit] "+s"(lit), [ns] "+s"(ns), [tb] "+s"(tb), [t0] "=&s"(t0), [t1] "=&s"(t1), \
+          [t2] "=&s"(t2), [t3] "=&s"(t3), [keep] "=&s"(keep), [tail] "+v"(tail), [dlo] "+v"(dlo), \
+          [dhi] "+v"(dhi), [vn] "=&v"(vn), [vy] "=&v"(vy), [vz] "=&v"(vz), [vd0] "=&v"(vd0), \
+          [vc2] "=&v"(vc2), [vcb] "=&v"(vcb), [val] "=&v"(val), [vah] "=&v"(vah), \
+          [vbl] "=&v"(vbl), [vbh] "=&v"(vbh) \
+        : [limit] "s"(limit), [mlimit] "s"(mlimit), [desc] "s"(desc), [lane4d] "v"(lane4d), \
+          [lane8] "v"(lane8) \
+        : "vcc", "scc", "memory")
+// x0 == x2 (bytes ip-2 .. ip+3 repeat with period 2): the table entry of ip
+// is the one ip-2 was just put into, so the candidate is ip-2 and the 4-byte
+// test passes -- a hit with offset 2, known without the table round trip; the
+// b-side window is the a-side window shifted by 2 bytes (a DPP lane shift)
+#define BSHUF_P2_BRANCH \
+        "s_cmp_eq_u32 %[t0], %[t1]\n\t" \
+        "s_cbranch_scc1 L_p2%=\n\t"
+#define BSHUF_P2_BLOCK \
+        "L_p2%=:\n\t" \
+        "s_and_b32 %[t3], %[ip], -4\n\t" \
+        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t" \
+        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t" \
+        "ds_read_b32 %[val], %[vcb]\n\t" \
+        "ds_read_b32 %[vah], %[vcb] offset:4\n\t" \
+        "s_lshr_b32 %[t0], %[t0], 18\n\t" \
+        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t" \
+        "v_mov_b32 %[vd0], %[ip]\n\t" \
+        "v_mov_b32 %[vz], %[t0]\n\t" \
+        "ds_write_b16 %[vz], %[vd0]\n\t" \
+        "s_and_b32 %[t3], %[ip], 3\n\t" \
+        "s_sub_u32 %[c2], %[ip], 2\n\t" \
+        "s_waitcnt lgkmcnt(1)\n\t" \
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t" \
+        "s_nop 1\n\t" \
+        "v_mov_b32_dpp %[vbh], %[tail] wave_shr:1 bound_ctrl:0\n\t" \
+        "v_alignbyte_b32 %[vbl], %[tail], %[vbh], 2\n\t" \
+        "v_writelane_b32 %[vbl], %[t1], 0\n\t" \
+        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t" \
+        "s_branch L_cmp%=\n\t"
+template <bool kP2>
+__device__ __forceinline__ int retest_chain(int& ip, int& ref, int& mc, int& lit, int& ns, int& tb,
+                                            uint32_t& tail, uint32_t& dlo, uint32_t& dhi, int& c2,
+                                            const int limit, const int mlimit, const uint32_t desc,
+                                            const uint32_t lane4d, const uint32_t lane8) {
+    int code;
+    int t0, t1, t2, t3, keep;
+    uint32_t vn, vy, vz, vd0, vc2, vcb, val, vah, vbl, vbh;
+    static_assert(kDescMax == 256, "the flush below hard-codes kDescMax");
+    if constexpr (kP2)
+        BSHUF_RETEST_ASM(BSHUF_P2_BRANCH, BSHUF_P2_BLOCK);
+    else
+        BSHUF_RETEST_ASM(, );
+    return code;
+}
+
 // Greedy LZ4 parse of D[0..n) with table T (zeroed).  Every sequence goes to
 // em.seq() once its match is final, the trailing literal run to em.last().
 // Returns the compressed size, or -1 when the emitter ran out of descriptor
@@ -511,6 +812,13 @@ template <bool WIDE, bool READBACK, int OPT, class Emit, class Blk>
 __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, Emit& em,
                                 const int lane) {
     DIAG_DECL
+    // the hand-scheduled re-test chain: LDS block (table at LDS 0, block at
+    // kTableBytes) with VGPR-buffered descriptors
+    constexpr bool kAsmRetest = !WIDE && !READBACK && std::is_same<Emit, EmitDescV>::value &&
+                                !std::is_same<Blk, GblBlk>::value;
+    // the hand-scheduled full search windows (OPT & 16384): LDS block too
+    constexpr bool kAsmSearch = !WIDE && !READBACK && (OPT & 16384) != 0 && (OPT & 512) == 0 &&
+                                !std::is_same<Blk, GblBlk>::value;
     int op = 0, anchor = 0;
     if (n >= kLz4MinLength) {
         const int limit = n - kMfLimit + 1;  // mflimitPlusOne
@@ -537,7 +845,29 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                     // path below.  A/B variant 512: every window general.
                     ProbeLane qs = probe_lane(kWave);
                     int k0 = 0;
-                    for (; p0 + qs.off <= limit; k0 += kWave) {
+                    if constexpr (kAsmSearch) {
+                        // the full windows by search_chain
+                        uint32_t vpos = (uint32_t)(p0 + q0.off - bias);
+                        uint32_t vnxt = (uint32_t)(p0 + q0.off + q0.step);
+                        uint32_t vstep = (uint32_t)(q0.step + kWave);
+                        uint32_t vseq = seq_cur, vcand = 0;
+                        int sqs = p0 + qs.off, sqstep = qs.step, nwin = 0, js = 0;
+                        const int code = search_chain(vpos, vnxt, vstep, vseq, sqs, sqstep, nwin, vcand, js,
+                                                      limit, n);
+                        if (code == kSrMatch) {
+                            const uint32_t cand = vcand & 0xFFFFu;
+                            mpos = __builtin_amdgcn_readlane((int)vpos, js);
+                            if (lane > js && cand <= (uint32_t)mpos) T.put(hash4(vseq), cand);
+                            mref = __builtin_amdgcn_readlane((int)cand, js);
+                            goto have_match;
+                        }
+                        // the partial window below: window nwin
+                        k0 = kWave * nwin;
+                        seq_cur = vseq;
+                        q0 = probe_lane(k0 + lane);
+                        bias = (k0 == 0 && lane == 0) ? 1 : 0;
+                    }
+                    for (; !kAsmSearch && p0 + qs.off <= limit; k0 += kWave) {
                         COUNT(1, 1);
                         const int pos = p0 + q0.off - bias;
                         const int pos_n = p0 + q0.off + q0.step;
@@ -697,6 +1027,59 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
             int ref = mref - co.back;
             int mc = co.back + co.cnt;
             STAMP(1);
+            if constexpr (kAsmRetest) {
+                // the hand-scheduled re-test chain (retest_chain); the rare
+                // cases it hands back are finished here
+                int lit = ip - anchor, tb = co.tail_base;
+                uint32_t tail = co.tail;
+                const uint32_t lane4d = (uint32_t)(uintptr_t)D + 4u * (uint32_t)lane;
+                const uint32_t lane8 = 8u * (uint32_t)lane;
+                const uint32_t desc_addr = (uint32_t)(uintptr_t)em.desc;
+                for (;;) {
+                    int c2 = 0;
+                    const int code = retest_chain<(OPT & 32768) != 0>(ip, ref, mc, lit, em.ns, tb, tail, em.dlo, em.dhi, c2,
+                                                  limit, mlimit, desc_addr, lane4d, lane8);
+                    anchor = ip;
+                    if (code == kRtLimit) goto last_literals;
+                    if (code == kRtMiss) break;
+                    if (code == kRtSlow) {
+                        // ip - 2 or ip + 3 outside the register window: from LDS
+                        const uint32_t h2 = hash4(lds_rd32(D, ip - 2)), h0 = hash4(lds_rd32(D, ip));
+                        T.put(h2, (uint32_t)(ip - 2));
+                        c2 = uni((int)T.get(h0));
+                        T.put(h0, (uint32_t)ip);
+                    }
+                    // kRtSlow: test and count; kRtLong: count on past the
+                    // first (all-equal) window -- from the window at ip
+                    uint32_t va = rdw(D, ip + 4 * lane, n), vb = rdw(D, c2 + 4 * lane, n);
+                    uint64_t ne = ballot(va != vb);
+                    if (ne & 1ull) break;
+                    int total = 0, c;
+                    for (;;) {
+                        c = kWinBytes;
+                        if (ne) {
+                            const int f = ffs64(ne);
+                            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)(va ^ vb), f);
+                            c = 4 * f + (__builtin_ctz(x) >> 3);
+                        }
+                        c = min(c, max(mlimit - (ip + total), 0));
+                        if (c < kWinBytes) break;
+                        total += kWinBytes;
+                        va = rdw(D, ip + total + 4 * lane, n);
+                        vb = rdw(D, c2 + total + 4 * lane, n);
+                        ne = ballot(va != vb);
+                    }
+                    tail = va;
+                    tb = ip + total;
+                    ref = c2;
+                    mc = total + c - kMinMatch;
+                    lit = 0;
+                }
+                // a miss: search from anchor + 1 (its first window's bytes)
+                pre = rdw(D, ip + 1 + lane, n);
+                ip = anchor + 1;
+                continue;
+            }
             for (;;) {
                 // ------------------------------------------------ emit sequence
                 if (!em.seq(op, anchor, ip, ip - ref, mc)) return -1;
@@ -1086,8 +1469,11 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         constexpr bool kDesc = !WIDE && (VAR & 2) == 0;
         if constexpr (kDesc) {
             if (a.desc_ok && 4 + lz4_bound(n) + 15 <= kTableBytes) {
-                EmitDesc em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048))>(D, n, T, em, lane);
+                // VAR & 8192: the hand-scheduled re-test chain, whose
+                // descriptors are buffered in VGPRs
+                using Em = typename std::conditional<(VAR & 8192) != 0, EmitDescV, EmitDesc>::type;
+                Em em{(lds32*)(D + a.desc_off), lane};
+                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768))>(D, n, T, em, lane);
                 KSTAMP(1);
                 if (em.ns > kDescMax) c = -1;  // more sequences than descriptor slots
                 if (c >= 0) {
@@ -1376,6 +1762,14 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 4096) return launch_enc_t<2, false, 4096>(a, nb, lds, s);
         if (v == 2048) return launch_enc_t<2, false, 2048>(a, nb, lds, s);
         if (v == 512) return launch_enc_t<2, false, 512>(a, nb, lds, s);
+    }
+    if constexpr (!WIDE && (VAR & ~256) == 0) {
+        // the hand-scheduled re-test chain, every element size (A/B 8192)
+        const int v = tuning_variant();
+        if (v == 8192) return launch_enc_t<EK, WIDE, VAR | 8192>(a, nb, lds, s);
+        if (v == 16384) return launch_enc_t<EK, WIDE, VAR | 16384>(a, nb, lds, s);
+        if (v == 24576) return launch_enc_t<EK, WIDE, VAR | 24576>(a, nb, lds, s);
+        if (v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);

@@ -5,18 +5,21 @@
 // whole block (src/bitshuffle.c:36-79; byU32 table + hash5 from 65547 bytes,
 // lz4/lz4.c:1388-1393).  The wave-per-block kernels keep the block (and the
 // encoder's 16 KiB table, the decoder's record) in LDS, which caps them at
-// max_lds_encode_bytes() / max_lds_decode_bytes().  Larger blocks take this
-// path instead:
+// max_lds_encode_bytes() / max_lds_decode_bytes().  Larger blocks take the
+// global-memory path:
 //   encode: bit transpose of every block into a global scratch (the
-//           k_bitshuffle kernels) -> one workgroup per block parses it with
-//           the table in global memory -> the usual offset scan + compaction;
-//   decode: the usual block index and token scan (k_seq_scan validates
-//           every record with LZ4_decompress_safe's exact checks) -> one
-//           workgroup per block executes the sequences into a global scratch
-//           -> inverse bit transpose into the output.
-// The parse and the copies run on lane 0 of each workgroup: these are the
-// rare, very large blocks (>= 80-144 KiB), correct first; the L2 keeps each
-// block's table and its working window close.
+//           k_bitshuffle kernels) -> k_lz4_encode_big (lz4_encode.hip): one
+//           wave per block runs the wave-parallel parse with the table in LDS
+//           and the block read from the scratch -> the usual offset scan +
+//           compaction;
+//   decode: the block index and k_seq_scan_big (one wave per block walks and
+//           validates every record with LZ4_decompress_safe's exact checks)
+//           -> k_lz4_exec_big (lz4_decode.hip): one wave per block executes
+//           the sequences wave-parallel into a global scratch -> inverse bit
+//           transpose into the output.
+// This file holds the launchers of that path and, as A/B variant 1024 only
+// (bshuf_set_variant), the round-2 kernels that parse and copy on lane 0 of
+// one workgroup per block with the table in global memory.
 #include "launch.h"
 
 namespace bshuf {

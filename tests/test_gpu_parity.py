@@ -136,11 +136,12 @@ def test_variant_knob_rejects_ablations(bs):
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
-    self-check fails), 2 the inline emitter (also the overflow path of the
+    self-check fails), 8192 the hand-scheduled re-test chain (asm, VGPR-buffered
+    descriptors), 2 the inline emitter (also the overflow path of the
     descriptor emitter), 4 the one-group-per-lane transpose, 8 the re-test
     table lookup by lane 0's returning exchange (the default: plain LDS ops by
     every lane); decoder record access: 16 straight from global memory with
@@ -166,6 +167,40 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
                 assert got.tobytes() == want.tobytes(), (arr.size, block)
                 back = bs.decompress_lz4(got, arr.shape, arr.dtype, block)
                 assert back.tobytes() == arr.tobytes(), (arr.size, block)
+    _with_variant(bs, variant, run)
+
+
+@pytest.mark.parametrize("variant", [8192, 16384, 24576, 40960])
+def test_encoder_variant_all_element_sizes(bs, oracle, variant):
+    """A variant that applies to every element size (8192: the hand-scheduled
+    re-test chain) on the oracle matrix of test_lz4_matches_oracle plus the
+    reference's regression chunks and the batch API."""
+    def run():
+        for kind in ("random", "runs", "periodic", "walk", "zeros"):
+            rng = np.random.default_rng(hash(kind) & 0xFFFF)
+            for E in [1, 2, 4, 8, 3, 12]:
+                for n in [13, 200, 5000, 40000]:
+                    nbytes = n * E
+                    if kind == "random":
+                        d = rng.integers(0, 256, nbytes, dtype=np.uint8)
+                    elif kind == "runs":
+                        d = np.repeat(rng.integers(0, 4, nbytes // 7 + 1), 7)[:nbytes].astype(np.uint8)
+                    elif kind == "periodic":
+                        d = (np.arange(nbytes) % (1 + (n % 13)) * 29).astype(np.uint8)
+                    elif kind == "walk":
+                        d = (rng.integers(-2, 3, nbytes).cumsum() % 256).astype(np.uint8)
+                    else:
+                        d = np.zeros(nbytes, dtype=np.uint8)
+                    arr = view_e(d, E)
+                    for block in [0, 64]:
+                        want = oracle.compress_lz4(arr, block)
+                        got = bs.compress_lz4(arr, block)
+                        assert got.tobytes() == want.tobytes(), (kind, E, n, block)
+        for ver, name, arr, chunk, block in regression_cases():
+            assert bs.compress_lz4(arr, block).tobytes() == chunk[12:].tobytes(), (ver, name)
+        for gen in (oracle.gen_g1, oracle.gen_g2):
+            a = gen(20 * 4096 + 1005)
+            assert bs.compress_lz4(a).tobytes() == oracle.compress_lz4(a).tobytes()
     _with_variant(bs, variant, run)
 
 
@@ -295,6 +330,15 @@ def test_device_decode_truncated_and_corrupt_headers(bs, oracle, torch):
             with pytest.raises(RuntimeError) as host:
                 bs.decompress_lz4(np.ascontiguousarray(buf), a.shape, a.dtype)
             assert host.value.args[1] == dev.value.args[1], i
+    # a zero-length last header: the reference's LZ4_decompress_safe returns -1
+    # for srcSize 0 without reading anything (-1001 from bshuf_decompress_lz4),
+    # so the oracle pins the host and device codes there
+    zero_last = bad[len(bad) - 2]
+    with pytest.raises(RuntimeError) as want:
+        oracle.decompress_lz4(np.ascontiguousarray(zero_last), a.shape, a.dtype)
+    with pytest.raises(RuntimeError) as host:
+        bs.decompress_lz4(np.ascontiguousarray(zero_last), a.shape, a.dtype)
+    assert want.value.args[1] == host.value.args[1] == -1001
 
 
 # ------------------------------------------------------------------ device API

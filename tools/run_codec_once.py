@@ -2,7 +2,7 @@
 data, for profilers.  Usage:
     python tools/run_codec_once.py [GiB] [enc|dec|both] [gen]
 gen 1 (default) = int16 G1 (config 2's data, seed 12345), 2 = float32 G2
-(config 3's data)."""
+(config 3's data).  BSHUF_VARIANT=v selects a byte-identical A/B variant."""
 import os
 import sys
 
@@ -17,6 +17,8 @@ what = sys.argv[2] if len(sys.argv) > 2 else "both"
 gen = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 dt = torch.int16 if gen == 1 else torch.float32
 n = int(gib * (1 << 30)) // torch.empty(0, dtype=dt).element_size()
+if os.environ.get("BSHUF_VARIANT"):  # byte-identical A/B variant (bshuf_set_variant)
+    assert B.lib.bshuf_set_variant(int(os.environ["BSHUF_VARIANT"])) == 0
 x = torch.empty(n, dtype=dt, device="cuda")
 B.synth_fill_dev(x, gen)
 c = api.compress_lz4_dev(x)
