@@ -1764,12 +1764,17 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 512) return launch_enc_t<2, false, 512>(a, nb, lds, s);
     }
     if constexpr (!WIDE && (VAR & ~256) == 0) {
-        // the hand-scheduled re-test chain, every element size (A/B 8192)
+        // default (byU16, every element size, single stream and batch): the
+        // hand-scheduled re-test chain with its offset-2 shortcut (8192 |
+        // 32768).  A/B variants: 65536 the compiled re-test (round 3's
+        // default), 8192 the chain without the shortcut, 16384 / 24576 the
+        // hand-scheduled search windows (alone / with the chain).
         const int v = tuning_variant();
+        if (v == 65536) return launch_enc_t<EK, WIDE, VAR | 65536>(a, nb, lds, s);
         if (v == 8192) return launch_enc_t<EK, WIDE, VAR | 8192>(a, nb, lds, s);
         if (v == 16384) return launch_enc_t<EK, WIDE, VAR | 16384>(a, nb, lds, s);
         if (v == 24576) return launch_enc_t<EK, WIDE, VAR | 24576>(a, nb, lds, s);
-        if (v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
+        if (v == 0 || v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);

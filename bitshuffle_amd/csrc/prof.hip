@@ -141,8 +141,9 @@ int bshuf_set_variant(int v) {
     // the re-test's 4-byte test by readfirstlane before the count, 4096 record
     // copy-out at the end of its block's parse (not deferred), 8192 the
     // hand-scheduled re-test chain, 16384 the hand-scheduled search windows,
-    // 24576 both, 40960 the re-test chain with its offset-2 shortcut
-    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 512 && v != 1024 && v != 2048 && v != 4096 && v != 8192 && v != 16384 && v != 24576 && v != 40960)
+    // 24576 both, 40960 the re-test chain with its offset-2 shortcut (the
+    // default for byU16 blocks), 65536 the compiled re-test chain
+    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 512 && v != 1024 && v != 2048 && v != 4096 && v != 8192 && v != 16384 && v != 24576 && v != 40960 && v != 65536)
         return -71;
     t_variant = v;
     return 0;

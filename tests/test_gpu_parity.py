@@ -136,12 +136,13 @@ def test_variant_knob_rejects_ablations(bs):
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960, 65536])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
     self-check fails), 8192 the hand-scheduled re-test chain (asm, VGPR-buffered
-    descriptors), 2 the inline emitter (also the overflow path of the
+    descriptors) without its offset-2 shortcut (40960 = the default), 65536 the
+    compiled re-test chain (round 3's default), 2 the inline emitter (also the overflow path of the
     descriptor emitter), 4 the one-group-per-lane transpose, 8 the re-test
     table lookup by lane 0's returning exchange (the default: plain LDS ops by
     every lane); decoder record access: 16 straight from global memory with
@@ -170,7 +171,7 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     _with_variant(bs, variant, run)
 
 
-@pytest.mark.parametrize("variant", [8192, 16384, 24576, 40960])
+@pytest.mark.parametrize("variant", [8192, 16384, 24576, 40960, 65536])
 def test_encoder_variant_all_element_sizes(bs, oracle, variant):
     """A variant that applies to every element size (8192: the hand-scheduled
     re-test chain) on the oracle matrix of test_lz4_matches_oracle plus the
