@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -85,7 +86,23 @@ size_t dec_ws(const Plan& p, int64_t blocks_end, int64_t in_nbytes, bool need_in
 // a process (round-2 host-path defect, DESIGN.md §4.2: 16 of 40 fresh HDF5
 // regression processes with the default pool, 0 of 40 with a pool that never
 // trims).  BSHUF_DIAG_POOL=default brings the default pool back for that
-// experiment only (tools/h5_repro.sh).
+// experiment only (tools/h5_repro.sh).  This is a WORKAROUND for re-mapping
+// behaviour whose mechanism is not understood, not a proven
+// root cause.  What the pool keeps is capped at the largest single workspace
+// requested so far (pool_keep): one call's worth stays mapped, not every
+// concurrent call's.
+std::atomic<uint64_t> g_pool_keep{0};
+bool g_pool_is_default = false;  // BSHUF_DIAG_POOL=default: leave its threshold alone
+void pool_keep(hipMemPool_t pool, size_t n) {
+    if (g_pool_is_default) return;
+    uint64_t cur = g_pool_keep.load(std::memory_order_relaxed);
+    while (cur < n && !g_pool_keep.compare_exchange_weak(cur, (uint64_t)n, std::memory_order_relaxed)) {
+    }
+    if (cur < n) {
+        uint64_t keep = g_pool_keep.load(std::memory_order_relaxed);
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+}
 hipMemPool_t workspace_pool() {
     static hipMemPool_t pool = nullptr;
     static bool tried = false;
@@ -98,6 +115,7 @@ hipMemPool_t workspace_pool() {
     const char* e = getenv("BSHUF_DIAG_POOL");
     if (e && !strcmp(e, "default")) {
         (void)hipDeviceGetDefaultMemPool(&pool, dev);
+        g_pool_is_default = true;
         return pool;
     }
     hipMemPoolProps props = {};
@@ -109,8 +127,6 @@ hipMemPool_t workspace_pool() {
         pool = nullptr;
         return nullptr;
     }
-    uint64_t keep = ~0ull;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     return pool;
 }
 
@@ -121,6 +137,7 @@ struct DevBuf {
         s = st;
         hipMemPool_t pool = workspace_pool();
         if (!pool) return hipErrorOutOfMemory;
+        pool_keep(pool, n ? n : 1);
         return hipMallocFromPoolAsync(&p, n ? n : 1, pool, st);
     }
     ~DevBuf() {

@@ -25,11 +25,33 @@ class ProfScope {
 };
 
 // Kernel-variant knob for A/B measurements (bshuf_set_variant, per thread,
-// byte-identical variants only); 0 = default.
+// byte-identical variants only); 0 = default.  The kNoPipe bit is not part of
+// the variant (pipe_ctx reads it).
 int tuning_variant();
 #ifdef BSHUF_DIAG
 int diag_variant();  // timing ablations (wrong output), diag build only
 #endif
+
+// Pipelined encode.  A long encode runs as kPipeSegs launches of the parse
+// kernel on the caller's stream, and each segment's offset scan + compaction
+// on a per-thread side stream as soon as that segment is parsed, so the
+// HBM-bound compaction overlaps the next segment's (LDS- and latency-bound)
+// parse.  pipe_ctx(s) returns the calling thread's side stream on
+// the current device and its fork / join events, or nullptr: pipelining off
+// (bshuf_set_variant bit kNoPipe), `s` being captured into a graph, or no
+// side stream.  Every fork is joined back into `s` before the call returns,
+// so callers see one stream-ordered operation as before.
+constexpr int kPipeSegs = 8;
+constexpr int64_t kPipeMinBlocks = 65536;  // shorter calls run unsegmented
+constexpr int kPipeEvents = kPipeSegs + 2;  // fork, one per segment, join
+constexpr int kNoPipe = 1 << 20;  // no pipelined encode
+struct PipeCtx {
+    hipStream_t side = nullptr;
+    hipEvent_t ev[kPipeEvents] = {};
+};
+PipeCtx* pipe_ctx(hipStream_t s);
+// s waits for everything enqueued on `from` so far (event ev)
+hipError_t stream_after(hipStream_t s, hipStream_t from, hipEvent_t ev);
 
 // Workgroups for a persistent launch: resident blocks per CU (occupancy API,
 // dynamic LDS included) x CUs of the current device, capped by the work.

@@ -572,6 +572,7 @@ struct DecArgs {
     const uint32_t* blk_seg;
     int32_t stage_off;  // EK == 0: LDS offset of the output staging block (0: none)
     int32_t ip_end;     // VAR & 512: the in-place record region ends at this LDS offset
+    int64_t blk0, blk1; // k_seq_scan / k_lz4_decode: this launch's blocks [blk0, blk1)
 };
 
 // Where block k lives: its stream's framed bytes, output, token-position area
@@ -824,8 +825,8 @@ struct SeqOut {
 // seq[offs[k]/3 + i] = payload position of sequence i's token (a sequence
 // takes >= 3 record bytes, so the per-block ranges are disjoint).
 __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
-    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k >= nb) return;
+    const int64_t k = a.blk0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= a.blk1) return;
     const BlockLoc loc = block_loc(a, k, nb, a.segs ? a.blk_seg[k] : 0u);
     const int n = loc.m * a.L.E;
     int64_t o0 = (int64_t)a.offs[k];
@@ -978,8 +979,9 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
         return kIP ? to_lds(smem) + a.ip_end - 16 * span_chunks(a, sp) : Cbuf;
     };
     const int64_t stride = gridDim.x;
-    int64_t blk = blockIdx.x;
-    if (blk >= nb) return;
+    int64_t blk = a.blk0 + blockIdx.x;
+    const int64_t end = a.blk1;  // this launch's blocks [blk0, end); nb: the whole stream(s)
+    if (blk >= end) return;
 
     PayRegsT<kIP ? kPayItersIP : kPayIters> R;
     // in place: every record is prefetched (partly, when long) into R
@@ -999,7 +1001,7 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
     uint32_t pref_pos = 0;  // kG: token position of block `next`, loaded a parse early
     constexpr bool kTouch = (VAR & 32) != 0;
     Touch t_cur{0u, 0u}, t_nxt{0u, 0u}, t_nxt2{0u, 0u};
-    if (next < nb) {
+    if (next < end) {
         nxt = span_from(a, issue_offs(a, next, nb, lane), nb);
         if constexpr (kG) {
             pref_pos = nxt.loc.seq[nxt.o0 / 3 + lane];
@@ -1010,7 +1012,7 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
         }
     }
     OffRegs O{0, 0};
-    if (next + stride < nb) O = issue_offs(a, next + stride, nb, lane);
+    if (next + stride < end) O = issue_offs(a, next + stride, nb, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
@@ -1053,20 +1055,20 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
         Span nxt2 = {};
         bool nxt2_in_regs = false;
         uint32_t nxt_pos = 0;
-        if (next < nb) {
+        if (next < end) {
             if constexpr (kG) {
                 nxt_pos = pref_pos;
-                if (nn < nb) {
+                if (nn < end) {
                     nxt2 = span_from(a, O, nb);
-                    if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                    if (nn + stride < end) O = issue_offs(a, nn + stride, nb, lane);
                     pref_pos = nxt2.loc.seq[nxt2.o0 / 3 + lane];
                     if constexpr (kTouch) t_nxt2 = touch_record(nxt2, lane);
                 }
             } else if constexpr (!kIP) {
                 nxt_pos = land_record(R, nxt_in_regs, a, nxt, Cbuf, lane);
-                if (nn < nb) {
+                if (nn < end) {
                     nxt2 = span_from(a, O, nb);
-                    if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                    if (nn + stride < end) O = issue_offs(a, nn + stride, nb, lane);
                     nxt2_in_regs = fits(nxt2);
                     if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
                 }
@@ -1147,13 +1149,13 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
         if constexpr (kIP) {
             // the decoded block has left LDS: the next record lands in place,
             // then the loads two ahead
-            if (next < nb) {
+            if (next < end) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 nxt_pos = land_record(R, nxt_in_regs, a, nxt, cbuf_of(nxt), lane);
-                if (nn < nb) {
+                if (nn < end) {
                     nxt2 = span_from(a, O, nb);
-                    if (nn + stride < nb) O = issue_offs(a, nn + stride, nb, lane);
+                    if (nn + stride < end) O = issue_offs(a, nn + stride, nb, lane);
                     nxt2_in_regs = fits(nxt2);
                     if (nxt2_in_regs) issue_pay(R, a, nxt2, lane);
                 }
@@ -1161,7 +1163,7 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (next >= nb) break;
+        if (next >= end) break;
         blk = next;
         cur = nxt;
         cur_pos = nxt_pos;
@@ -1430,9 +1432,10 @@ hipError_t scan_big_impl(DecArgs& a, int64_t nb, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t scan_impl(DecArgs& a, int64_t nb, hipStream_t s) {
+// token scan of blocks [a.blk0, a.blk1) (nb: all blocks of the stream(s))
+hipError_t scan_impl(const DecArgs& a, int64_t nb, hipStream_t s) {
     ProfScope prof("k_seq_scan", s);
-    hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, a, nb);
+    hipLaunchKernelGGL(k_seq_scan, dim3((unsigned)((a.blk1 - a.blk0 + 255) / 256)), dim3(256), 0, s, a, nb);
     return hipGetLastError();
 }
 
@@ -1488,8 +1491,7 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
         default: fn = inplace ? BSHUF_DEC(0, 512) : touch ? BSHUF_DEC(0, 48) : (grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0)); break;
     }
 #undef BSHUF_DEC
-    hipError_t e = scan_impl(a, nb, s);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
 #if defined(BSHUF_DIAG) || defined(BSHUF_OCC)
     // occupancy experiment: BSHUF_DIAG_DEC_WAVES=w pads the LDS request so
     // that at most w waves fit a CU
@@ -1502,12 +1504,24 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    const dim3 grid((unsigned)persistent_grid(fn, kWave, lds, nb));
-    ProfScope prof("k_lz4_decode", s);
-    void* args[] = {&a, const_cast<int64_t*>(&nb)};
-    e = hipLaunchKernel(fn, grid, dim3(kWave), args, lds, s);
-    if (e != hipSuccess) return e;
-    return hipGetLastError();
+    // blocks [f0, f1) on stream st (DecArgs carries the range)
+    auto dec = [&](int64_t f0, int64_t f1, hipStream_t st) -> hipError_t {
+        DecArgs aa = a;
+        aa.blk0 = f0;
+        aa.blk1 = f1;
+        const dim3 grid((unsigned)persistent_grid(fn, kWave, lds, f1 - f0));
+        ProfScope prof("k_lz4_decode", st);
+        void* args[] = {&aa, const_cast<int64_t*>(&nb)};
+        hipError_t r = hipLaunchKernel(fn, grid, dim3(kWave), args, lds, st);
+        return r != hipSuccess ? r : hipGetLastError();
+    };
+    // (the scan stays ahead of the whole decode: run beside it in segments on a
+    // side stream, it slowed the issue-bound decoder more than it hid,
+    // 4.20 -> 4.24 ms G1 / 8.00 -> 8.21 ms G2 per 4 GiB, profiles/r04/pipe)
+    a.blk0 = 0;
+    a.blk1 = nb;
+    e = scan_impl(a, nb, s);
+    return e != hipSuccess ? e : dec(0, nb, s);
 }
 
 // Batch result per stream: bytes consumed, or the error of its LAST failing
@@ -1540,7 +1554,7 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
                   (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr,
-                  ((uintptr_t)out & 7) == 0 ? 1 : 0};
+                  ((uintptr_t)out & 7) == 0 ? 1 : 0, 0, 0, nb};
         if (nmax > max_lds_decode_bytes()) {
             // large blocks: validated by the same scan (a wave per block),
             // executed in global memory
@@ -1572,7 +1586,7 @@ hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
             al8 = al8 && ((uintptr_t)hsegs[i].out & 7) == 0;
         }
         DecArgs a{nullptr, 0, b.offs, nullptr, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg, al8 ? 1 : 0};
+                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg, al8 ? 1 : 0, 0, 0, nb};
         e = decode_impl(a, nb, aligned, s);
         if (e != hipSuccess) return e;
     }

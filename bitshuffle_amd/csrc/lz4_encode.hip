@@ -109,6 +109,7 @@ struct EncArgs {
     const Seg* segs;   // batch: per-stream table (nullptr: the single stream in/L)
     const uint32_t* blk_seg;
     int32_t raw8;      // EK == 0: every block source is 8-aligned (LDS-staged transpose)
+    int64_t blk0;      // batch: global index of this launch's block 0 (pipelined segments)
 };
 
 // Returning LDS atomics as inline asm (no builtin exists for ds_mskor); the
@@ -1301,6 +1302,8 @@ __device__ __forceinline__ void raw_to_lds(const RawRegs& R, lds8* S, int nbytes
 template <int EK, bool WIDE, int VAR>
 __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // issue priority over a concurrent compaction's waves (pipelined encode)
+    __builtin_amdgcn_s_setprio(2);
     const int lane = threadIdx.x;
     const int E = EK ? EK : a.L.E;
     (void)smem;
@@ -1313,13 +1316,13 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     constexpr bool kBatch = (VAR & 256) != 0;
     auto blk_m = [&](int64_t k) {
         if (!kBatch) return k < a.L.nfull ? a.L.bs : a.L.last;
-        const Seg& g = a.segs[a.blk_seg[k]];
-        return k - g.first < g.nfull ? a.L.bs : g.last;
+        const Seg& g = a.segs[a.blk_seg[k + a.blk0]];
+        return k + a.blk0 - g.first < g.nfull ? a.L.bs : g.last;
     };
     auto blk_src = [&](int64_t k) {
         if (!kBatch) return a.in + k * (int64_t)a.L.bs * E;
-        const Seg& g = a.segs[a.blk_seg[k]];
-        return g.in + (k - g.first) * (int64_t)a.L.bs * E;
+        const Seg& g = a.segs[a.blk_seg[k + a.blk0]];
+        return g.in + (k + a.blk0 - g.first) * (int64_t)a.L.bs * E;
     };
 
     BlockRegs<EK> R;
@@ -1526,7 +1529,8 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
 // stores it whole -- or, for the <= 2 edge chunks a record shares with its
 // neighbours, byte by byte from the same registers.  Up to kCompactUnroll
 // chunks per lane are loaded before any is stored.  One WAVE per record, four
-// records per 256-thread workgroup.
+// records per 256-thread workgroup; records first .. nb-1 (a pipelined
+// segment, or all).
 constexpr int kCompactPerWg = 4;
 constexpr int kCompactUnroll = 4;
 
@@ -1556,8 +1560,9 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ scr
                                                  const uint64_t* __restrict__ offs,
                                                  uint8_t* __restrict__ out, const Seg* segs,
                                                  const uint32_t* __restrict__ blk_seg,
-                                                 uint64_t* __restrict__ block_offsets, int64_t nb) {
-    const int64_t blk = (int64_t)blockIdx.x * kCompactPerWg + (threadIdx.x >> 6);
+                                                 uint64_t* __restrict__ block_offsets, int64_t first,
+                                                 int64_t nb) {
+    const int64_t blk = first + (int64_t)blockIdx.x * kCompactPerWg + (threadIdx.x >> 6);
     const int tid = threadIdx.x & 63;
     if (blk >= nb) return;
     uint64_t rel0 = offs[blk];
@@ -1808,6 +1813,54 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
 
 int64_t max_device_block_bytes() { return 160 * 1024 - kTableBytes - 64; }
 
+namespace {
+
+// Pipelined encode (launch.h): parse segment i on s (enc(f_i, f_i+1)), then on
+// the side stream, as soon as it is parsed, the offset scan over blocks
+// [0, f_i+1) and the compaction of [f_i, f_i+1) -- overlapping the parse of
+// later segments (whose waves raise their issue priority, s_setprio, so the
+// compaction takes the issue slots the parse's dependency chain leaves idle).
+// The scan (hipcub) needs LDS, which a running parse holds on every CU, so it
+// starts as a parse segment drains, and the compaction behind it fills the
+// drain: measured on one box (profiles/r04/pipe), 4 GiB G1 compress 11.47 ->
+// 11.12 ms with 8 segments, 11.14 with 4; an LDS-free one-wave scan that let
+// the compaction run beside the parse body instead gained only 11.47 -> 11.25 /
+// 11.38 ms.  The scan of segment i reads foot[f_i+1], which segment i+1 may be
+// writing; that element feeds no output of the scan.  foot[nb] = 0 before the
+// fork.  The side stream joins s before `finish` runs on s.
+template <class Enc, class Fin>
+hipError_t encode_pipelined(int64_t nb, hipStream_t s, PipeCtx* pc, const EncodeBufs& b, Enc enc,
+                            uint8_t* out, const Seg* segs, const uint32_t* blk_seg,
+                            uint64_t* block_offsets, Fin finish) {
+    hipError_t e = dev_fill(b.foot + nb, 0, sizeof(uint64_t), s);
+    if (e == hipSuccess) e = stream_after(pc->side, s, pc->ev[0]);
+    for (int i = 0; i < kPipeSegs && e == hipSuccess; i++) {
+        const int64_t f0 = nb * i / kPipeSegs, f1 = nb * (i + 1) / kPipeSegs;
+        if (f1 == f0) continue;
+        e = enc(f0, f1);
+        if (e == hipSuccess) e = stream_after(pc->side, s, pc->ev[1 + i]);
+        if (e != hipSuccess) break;
+        {
+            size_t tmp = b.scan_tmp_bytes;
+            ProfScope prof("scan_block_offsets", pc->side);
+            e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.foot, b.offs, (int)(f1 + 1), pc->side);
+        }
+        if (e != hipSuccess) break;
+        ProfScope prof("k_compact", pc->side);
+        hipLaunchKernelGGL(k_compact, dim3((unsigned)((f1 - f0 + kCompactPerWg - 1) / kCompactPerWg)),
+                           dim3(256), 0, pc->side, b.scratch, b.slot, b.offs, out, segs, blk_seg,
+                           block_offsets, f0, f1);
+        e = hipGetLastError();
+    }
+    // join even after an error, so nothing of this call is left on the side stream unordered
+    const hipError_t j = stream_after(s, pc->side, pc->ev[kPipeEvents - 1]);
+    if (e != hipSuccess) return e;
+    if (j != hipSuccess) return j;
+    return finish(s);
+}
+
+}  // namespace
+
 hipError_t launch_encode_big(const uint8_t* shuf, const Layout& L, const EncodeBufs& b, hipStream_t s) {
     if (L.nblocks() == 0) return hipSuccess;
     return lds_atomics_lane_ordered() ? launch_big_t<false>(shuf, L, b, s) : launch_big_t<true>(shuf, L, b, s);
@@ -1872,6 +1925,16 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
 #undef BSHUF_E
             return hipErrorInvalidValue;
         };
+        PipeCtx* pc = (wide == wide_last || !L.last) && nb >= kPipeMinBlocks ? pipe_ctx(s) : nullptr;
+        if (pc) return encode_pipelined(nb, s, pc, b, [&](int64_t f0, int64_t f1) {
+            return go(L, wide, f1 - f0, f0);
+        }, out, nullptr, nullptr, nullptr, [&](hipStream_t st) {
+            const uint8_t* tail_src = in + (L.nfull * (int64_t)L.bs + L.last) * L.E;
+            ProfScope prof("k_encode_finish", st);
+            hipLaunchKernelGGL(k_encode_finish, dim3(1), dim3(64), 0, st, b.offs, nb, tail_src, tail_bytes,
+                               out, d_result);
+            return hipGetLastError();
+        });
         if (wide == wide_last || !L.last) {
             e = go(L, wide, nb, 0);
         } else {
@@ -1894,7 +1957,7 @@ hipError_t launch_encode(const uint8_t* in, uint8_t* out, const Layout& L, int64
         ProfScope prof("k_compact", s);
         hipLaunchKernelGGL(k_compact, dim3((unsigned)((nb + kCompactPerWg - 1) / kCompactPerWg)),
                            dim3(256), 0, s, b.scratch, b.slot, b.offs, out, (const Seg*)nullptr,
-                           (const uint32_t*)nullptr, (uint64_t*)nullptr, nb);
+                           (const uint32_t*)nullptr, (uint64_t*)nullptr, (int64_t)0, nb);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1926,20 +1989,37 @@ hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
         bool aligned = true;
         for (int i = 0; i < nsegs; i++) aligned = aligned && ((uintptr_t)hsegs[i].in & 15) == 0;
         const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
+        // blocks [f0, f1) of the batch: the segment table is indexed globally
+        // (blk0), scratch slots and sizes relative to f0
+        auto go = [&](int64_t f0, int64_t f1) -> hipError_t {
+            EncArgs aa = a;
+            aa.blk0 = f0;
+            aa.scratch = a.scratch + f0 * b.slot;
+            aa.foot = a.foot + f0;
+            const int64_t cnt = f1 - f0;
 #define BSHUF_E(EKV)                                                                  \
     case EKV:                                                                         \
-        e = wide ? launch_enc_t<EKV, true, 256>(a, nb, lds, s)                        \
-                 : launch_enc_t<EKV, false, 256>(a, nb, lds, s);                      \
-        break;
-        switch (ek) {
-            BSHUF_E(0)
-            BSHUF_E(1)
-            BSHUF_E(2)
-            BSHUF_E(4)
-            BSHUF_E(8)
-            default: e = hipErrorInvalidValue;
-        }
+        return wide ? launch_enc_t<EKV, true, 256>(aa, cnt, lds, s)                   \
+                    : launch_enc_t<EKV, false, 256>(aa, cnt, lds, s);
+            switch (ek) {
+                BSHUF_E(0)
+                BSHUF_E(1)
+                BSHUF_E(2)
+                BSHUF_E(4)
+                BSHUF_E(8)
+            }
 #undef BSHUF_E
+            return hipErrorInvalidValue;
+        };
+        PipeCtx* pc = nb >= kPipeMinBlocks ? pipe_ctx(s) : nullptr;
+        if (pc) return encode_pipelined(nb, s, pc, b, go, nullptr, segs, blk_seg, block_offsets,
+                                        [&](hipStream_t st) {
+            ProfScope prof("k_encode_finish", st);
+            hipLaunchKernelGGL(k_encode_finish_batch, dim3((unsigned)nsegs), dim3(64), 0, st, b.offs, segs,
+                               L.bs, L.E);
+            return hipGetLastError();
+        });
+        e = go(0, nb);
         if (e != hipSuccess) return e;
     }
     e = dev_fill(b.foot + nb, 0, sizeof(uint64_t), s);
@@ -1954,7 +2034,7 @@ hipError_t launch_encode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
         ProfScope prof("k_compact", s);
         hipLaunchKernelGGL(k_compact, dim3((unsigned)((nb + kCompactPerWg - 1) / kCompactPerWg)),
                            dim3(256), 0, s, b.scratch, b.slot, b.offs, (uint8_t*)nullptr, segs,
-                           blk_seg, block_offsets, nb);
+                           blk_seg, block_offsets, (int64_t)0, nb);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

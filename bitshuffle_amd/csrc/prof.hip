@@ -58,7 +58,51 @@ bool prof_on() { return P().on; }
 // A/B knob: per calling thread, and only byte-identical variants are accepted
 // (the timing ablations that change the output exist in the diag build only).
 static thread_local int t_variant = 0;
-int tuning_variant() { return t_variant; }
+int tuning_variant() { return t_variant & ~kNoPipe; }
+
+namespace {
+// The calling thread's side streams, one per device (kept for the thread's
+// life; the destructor waits for them, ignoring errors at process exit).
+constexpr int kPipeDevices = 16;
+struct PipeSet {
+    PipeCtx c[kPipeDevices];
+    bool bad[kPipeDevices] = {};
+    ~PipeSet() {
+        for (PipeCtx& x : c) {
+            if (!x.side) continue;
+            (void)hipStreamSynchronize(x.side);
+            for (hipEvent_t& e : x.ev)
+                if (e) (void)hipEventDestroy(e);
+            (void)hipStreamDestroy(x.side);
+        }
+    }
+};
+thread_local PipeSet t_pipe;
+}  // namespace
+
+PipeCtx* pipe_ctx(hipStream_t s) {
+    if (t_variant & kNoPipe) return nullptr;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kPipeDevices || t_pipe.bad[dev]) return nullptr;
+    PipeCtx& x = t_pipe.c[dev];
+    if (x.side) return &x;
+    bool ok = hipStreamCreateWithFlags(&x.side, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; ok && i < kPipeEvents; i++)
+        ok = hipEventCreateWithFlags(&x.ev[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        t_pipe.bad[dev] = true;  // leaked: at most once per thread and device
+        x = PipeCtx{};
+        return nullptr;
+    }
+    return &x;
+}
+
+hipError_t stream_after(hipStream_t s, hipStream_t from, hipEvent_t ev) {
+    hipError_t e = hipEventRecord(ev, from);
+    return e == hipSuccess ? hipStreamWaitEvent(s, ev, 0) : e;
+}
 #ifdef BSHUF_DIAG
 static int g_diag_variant = 0;
 int diag_variant() { return g_diag_variant; }
@@ -142,8 +186,10 @@ int bshuf_set_variant(int v) {
     // copy-out at the end of its block's parse (not deferred), 8192 the
     // hand-scheduled re-test chain, 16384 the hand-scheduled search windows,
     // 24576 both, 40960 the re-test chain with its offset-2 shortcut (the
-    // default for byU16 blocks), 65536 the compiled re-test chain
-    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128 && v != 512 && v != 1024 && v != 2048 && v != 4096 && v != 8192 && v != 16384 && v != 24576 && v != 40960 && v != 65536)
+    // default for byU16 blocks), 65536 the compiled re-test chain; any of
+    // them | kNoPipe (1 << 20): no pipelined encode (launch.h)
+    const int vv = v & ~kNoPipe;
+    if (vv != 0 && vv != 2 && vv != 4 && vv != 8 && vv != 16 && vv != 32 && vv != 64 && vv != 128 && vv != 512 && vv != 1024 && vv != 2048 && vv != 4096 && vv != 8192 && vv != 16384 && vv != 24576 && vv != 40960 && vv != 65536)
         return -71;
     t_variant = v;
     return 0;

@@ -467,6 +467,66 @@ def test_device_api_unaligned_pointers(bs, oracle, torch):
         assert sh[off_out:off_out + nbytes].cpu().numpy().tobytes() == oracle.bitshuffle(a).tobytes()
 
 
+# --------------------------------------------------------- pipelined encode
+NO_PIPE = 1 << 20  # bshuf_set_variant bit: encode without segments / side stream
+
+
+def test_pipelined_encode_matches_oracle(bs, oracle, torch):
+    """Encodes of >= 65536 blocks run as 4 parse segments with each segment's
+    offset scan + compaction on a side stream (launch.h).  Single stream:
+    65536 + 3 full blocks (not a multiple of 4), a partial block and a raw
+    tail, caller workspace and ws = NULL; batch: 19 streams of uneven sizes
+    whose segment boundaries fall inside streams.  Every stream equals the
+    oracle's and the unsegmented (NO_PIPE) encode's, offsets included."""
+    import ctypes
+    n = (65536 + 3) * 4096 + 1005 + 5
+    a = oracle.gen_g1(n, 0, 4321)
+    want = oracle.compress_lz4(a)
+    x = torch.from_numpy(a).cuda()
+    nb = int(bs.lib.bshuf_lz4_dev_nblocks(n, 2, 0))
+    got = {}
+    for v in (0, NO_PIPE):
+        def run():
+            outs = []
+            for ws in (True, False):
+                out = torch.empty(bs.compress_lz4_bound(n, 2, 0), dtype=torch.uint8, device="cuda")
+                res = torch.empty(1, dtype=torch.int64, device="cuda")
+                off = torch.zeros(nb, dtype=torch.int64, device="cuda")
+                wsb = int(bs.lib.bshuf_compress_lz4_dev_workspace(n, 2, 0))
+                w = torch.empty(wsb, dtype=torch.uint8, device="cuda") if ws else None
+                rc = bs.lib.bshuf_compress_lz4_dev(
+                    ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, 2, 0,
+                    ctypes.c_void_p(w.data_ptr()) if ws else None, wsb if ws else 0,
+                    ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(off.data_ptr()), None)
+                assert rc == 0
+                c = int(res.item())
+                outs.append((out[:c].cpu().numpy().tobytes(), off.cpu().numpy().copy()))
+            return outs
+        got[v] = _with_variant(bs, v, run)
+    for v in got:
+        for enc, off in got[v]:
+            assert enc == want.tobytes(), v
+            assert np.array_equal(off, got[NO_PIPE][0][1]), v
+    del x
+    # batch above the threshold: uneven streams
+    sizes = [(3000 + 577 * i) * 4096 + 37 * i for i in range(19)]
+    arrs = [oracle.gen_g1(m, 7 * i, 99 + i) for i, m in enumerate(sizes)]
+    xs = [torch.from_numpy(q).cuda() for q in arrs]
+    nblk = sum(int(bs.lib.bshuf_lz4_dev_nblocks(q.size, 2, 0)) for q in arrs)
+    assert nblk >= 65536
+    res = {}
+    for v in (0, NO_PIPE):
+        def runb():
+            offs = torch.zeros(nblk, dtype=torch.int64, device="cuda")
+            outs = bs.compress_lz4_batch_dev(xs, 0, offsets=offs)
+            return [o.cpu().numpy().tobytes() for o in outs], offs.cpu().numpy()
+        res[v] = _with_variant(bs, v, runb)
+    for q, enc in zip(arrs, res[0][0]):
+        assert enc == oracle.compress_lz4(q).tobytes(), q.size
+    assert res[0][0] == res[NO_PIPE][0]
+    assert np.array_equal(res[0][1], res[NO_PIPE][1])
+
+
 # ------------------------------------------------------------------ batch API
 def test_batch_api_matches_oracle(bs, oracle, torch):
     """bshuf_*_lz4_batch_dev: streams of different lengths (partial blocks,
