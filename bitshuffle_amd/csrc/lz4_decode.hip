@@ -570,7 +570,8 @@ struct DecArgs {
     uint32_t* seq;   // token positions (k_seq_scan -> lz4_exec_block)
     const Seg* segs; // batch: per-stream table (nullptr: the single stream above)
     const uint32_t* blk_seg;
-    int32_t stage_off;  // EK == 0: LDS offset of the output staging block (0: none)
+    int32_t stage_off;  // EK == 0: LDS offset of the output staging block (0: none,
+                        // -1: through registers into the block's own LDS)
     int32_t ip_end;     // VAR & 512: the in-place record region ends at this LDS offset
     int64_t blk0, blk1; // k_seq_scan / k_lz4_decode: this launch's blocks [blk0, blk1)
 };
@@ -1111,6 +1112,45 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
                     }
                     store_group<EK>(dst + (int64_t)g * 8 * EK, w);
                 }
+            } else if (a.stage_off < 0) {
+                // any element size, blocks of <= 8 KiB (every default block
+                // size): the inverse transpose of all the block's (group,
+                // byte) items into registers (16 per lane), then their bytes
+                // back over the block's own LDS in raw element order, then
+                // coalesced 8-byte stores.  No staging buffer: the decoder
+                // keeps 18 resident waves per CU (a staged 8 KiB block needs
+                // 14 LDS granules instead of 7: 9 waves).
+                constexpr int kRegItems = 8192 / 8 / kWave;
+                const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)E - 1) / (uint64_t)E);
+                const int items = P * E;  // 8-byte words of the block, <= 1024
+                uint64_t v[kRegItems];
+#pragma unroll
+                for (int r = 0; r < kRegItems; r++) {
+                    const int i = lane + kWave * r;
+                    v[r] = 0;
+                    if (i < items) {
+                        const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                        uint64_t x = 0;
+#pragma unroll
+                        for (int j = 0; j < 8; j++) x |= (uint64_t)D[(8 * b + j) * P + g] << (8 * j);
+                        v[r] = tr8x8(x);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < kRegItems; r++) {
+                    const int i = lane + kWave * r;
+                    if (i < items) {
+                        const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                        lds8* y = D + 8 * g * E + b;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) y[k * E] = (uint8_t)(v[r] >> (8 * k));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                for (int i = lane; i < items; i += kWave) ((gbl64*)dst)[i] = ((const lds64v*)D)[i];
             } else if (a.stage_off) {
                 // any element size: inverse transpose into an LDS staging
                 // block, then coalesced 8-byte stores (outputs 8-aligned)
@@ -1455,9 +1495,13 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     a.ip_end = (int32_t)(((size_t)a.cap + kInPlaceMargin + 15) & ~(size_t)15);
     size_t lds = inplace ? (size_t)a.ip_end + 32 : (size_t)a.cap + 16 + (grec ? 0 : rec);
     const int ek = aligned && (L.E == 1 || L.E == 2 || L.E == 4 || L.E == 8) ? L.E : 0;
-    // any other element size: stage the inverse transpose in LDS when every
-    // output is 8-aligned (a.stage_off was set to 1 by the caller as "may")
-    if (ek == 0 && a.stage_off) {
+    // any other element size: stage the inverse transpose when every output
+    // is 8-aligned (a.stage_off was set to 1 by the caller as "may") -- through
+    // registers for blocks of <= 8 KiB (stage_off -1), else in an LDS block of
+    // its own
+    if (ek == 0 && a.stage_off && (int64_t)L.bs * L.E <= 8192) {
+        a.stage_off = -1;
+    } else if (ek == 0 && a.stage_off) {
         a.stage_off = (int32_t)lds;
         lds += (size_t)a.cap;
     } else {
