@@ -162,16 +162,15 @@ __device__ __forceinline__ void scatter_byte_plane(uint32_t (&w)[2 * EK], int b,
 }
 
 // Bit-sliced inverse transpose of FOUR consecutive groups (4q .. 4q+3) of a
-// block: pl[r] holds byte (4q + k) of plane r in its byte k (one LDS dword per
-// plane).  The 8x8 bit transposes of all four groups run at once, as three
-// swap stages between plane registers (bits of one byte never leave it):
-// after them x[8b + i] byte k = byte b of element 8(4q + k) + i.  out[] gets
-// the 32 * EK contiguous output bytes of the four groups.
+// block, in place: x[r] holds byte (4q + k) of plane r in its byte k (one LDS
+// dword per plane).  The 8x8 bit transposes of all four groups run at once, as
+// three swap stages between plane registers (bits of one byte never leave it):
+// after them x[8b + i] byte k = byte b of element 8(4q + k) + i, and
+// untranspose4_word(x, w) composes output dword w of the 32 * EK contiguous
+// bytes of the four groups -- word by word, so a caller can store each 16 bytes
+// as they are made and keep only x live (EK = 4: 32 registers, not 96).
 template <int EK>
-__device__ __forceinline__ void untranspose4(const uint32_t (&pl)[8 * EK], uint32_t (&out)[8 * EK]) {
-    uint32_t x[8 * EK];
-#pragma unroll
-    for (int r = 0; r < 8 * EK; r++) x[r] = pl[r];
+__device__ __forceinline__ void untranspose4_rows(uint32_t (&x)[8 * EK]) {
 #pragma unroll
     for (int b = 0; b < EK; b++) {
         uint32_t* y = x + 8 * b;
@@ -195,19 +194,20 @@ __device__ __forceinline__ void untranspose4(const uint32_t (&pl)[8 * EK], uint3
             y[j] ^= t << 4;
         }
     }
-    // output byte o = (8k + i) * EK + b  <-  x[8b + i] byte k
+}
+
+// output byte o = (8k + i) * EK + b  <-  x[8b + i] byte k
+template <int EK>
+__device__ __forceinline__ uint32_t untranspose4_word(const uint32_t (&x)[8 * EK], const int w) {
+    uint32_t v = 0;
 #pragma unroll
-    for (int w = 0; w < 8 * EK; w++) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int o = 4 * w + t;
-            const int b = o % EK, e = o / EK;
-            const int k = e >> 3, i = e & 7;
-            v |= ((x[8 * b + i] >> (8 * k)) & 0xFFu) << (8 * t);
-        }
-        out[w] = v;
+    for (int t = 0; t < 4; t++) {
+        const int o = 4 * w + t;
+        const int b = o % EK, e = o / EK;
+        const int k = e >> 3, i = e & 7;
+        v |= ((x[8 * b + i] >> (8 * k)) & 0xFFu) << (8 * t);
     }
+    return v;
 }
 
 template <int EK>

@@ -959,7 +959,7 @@ __device__ __forceinline__ uint32_t land_record(const PayRegsT<IT>& R, bool in_r
 // the completion of the previous block's stores (gfx9 counts loads and stores
 // on one in-order vmcnt) stalls the wave.
 template <int EK, int VAR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 4 ? 4 : 5) : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 4 || EK == 0 ? 4 : 5) : 1)))
 void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
@@ -1090,14 +1090,15 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
                 const int P4 = (EK <= 4 && (P & 3) == 0) ? P >> 2 : 0;
                 const lds32* D32 = (const lds32*)D;
                 for (int q = lane; q < P4; q += kWave) {
-                    uint32_t pl[8 * EK], ob[8 * EK];
+                    uint32_t x[8 * EK];
 #pragma unroll
-                    for (int r = 0; r < 8 * EK; r++) pl[r] = D32[r * P4 + q];
-                    untranspose4<EK>(pl, ob);
+                    for (int r = 0; r < 8 * EK; r++) x[r] = D32[r * P4 + q];
+                    untranspose4_rows<EK>(x);
                     uint4* o4 = reinterpret_cast<uint4*>(dst + (int64_t)q * 32 * EK);
 #pragma unroll
                     for (int v = 0; v < 2 * EK; v++)
-                        o4[v] = make_uint4(ob[4 * v], ob[4 * v + 1], ob[4 * v + 2], ob[4 * v + 3]);
+                        o4[v] = make_uint4(untranspose4_word<EK>(x, 4 * v), untranspose4_word<EK>(x, 4 * v + 1),
+                                           untranspose4_word<EK>(x, 4 * v + 2), untranspose4_word<EK>(x, 4 * v + 3));
                 }
                 for (int g = (P4 ? P : lane); g < P; g += kWave) {
                     uint32_t w[2 * EK];
