@@ -1021,6 +1021,7 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
             STAMP(0);
             if (mpos < 0) break;
         have_match:
+            STAMP(0);  // (the search's match exits jump here)
             COUNT(0, 1);
             // ------------------------------------------------ catch up + count
             CountOut co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
@@ -1041,7 +1042,10 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                     const int code = retest_chain<(OPT & 32768) != 0>(ip, ref, mc, lit, em.ns, tb, tail, em.dlo, em.dhi, c2,
                                                   limit, mlimit, desc_addr, lane4d, lane8);
                     anchor = ip;
-                    if (code == kRtLimit) goto last_literals;
+                    if (code == kRtLimit) {
+                        STAMP(4);
+                        goto last_literals;
+                    }
                     if (code == kRtMiss) break;
                     if (code == kRtSlow) {
                         // ip - 2 or ip + 3 outside the register window: from LDS
@@ -1076,7 +1080,10 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                     mc = total + c - kMinMatch;
                     lit = 0;
                 }
-                // a miss: search from anchor + 1 (its first window's bytes)
+                STAMP(4);
+                // a miss: search from anchor + 1 (its first window's bytes;
+                // read beside every re-test's table ops instead, variant
+                // 172032 in round 4: no change on G1 / G2 / E = 3 / E = 12)
                 pre = rdw(D, ip + 1 + lane, n);
                 ip = anchor + 1;
                 continue;

@@ -1,5 +1,5 @@
 """Phase split of k_lz4_encode from the diagnostic build (BSHUF_DIAG stamps).
-Usage: python tools/diag_encode.py [GiB]   (runs on the GPU box)"""
+Usage: python tools/diag_encode.py [GiB] [gen] [elem_size]   (runs on the GPU box)"""
 import ctypes
 import os
 import sys
@@ -13,17 +13,20 @@ from bitshuffle_amd import api  # noqa: E402
 
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
 gen = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+es = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # element size override (the same bytes)
 n = int(gib * (1 << 30)) // (2 if gen == 1 else 4)
 x = torch.empty(n, dtype=torch.int16 if gen == 1 else torch.float32, device="cuda")
 B.synth_fill_dev(x, gen)
+if es:
+    x = x.view(torch.uint8)[: (x.numel() * x.element_size() // es) * es]
 rd = B.lib.bshuf_diag_read
 rd.argtypes = [ctypes.c_void_p]
 buf = (ctypes.c_ulonglong * 32)()
-c = api.compress_lz4_dev(x)
+c = api.compress_lz4_dev(x, elem_size=es or None)
 torch.cuda.synchronize()
 rd(buf)  # reset after warm-up
 B.lib.bshuf_prof_enable(1)
-c = api.compress_lz4_dev(x)
+c = api.compress_lz4_dev(x, elem_size=es or None)
 torch.cuda.synchronize()
 rd(buf)
 import bench  # noqa: E402
