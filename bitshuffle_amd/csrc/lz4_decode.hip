@@ -36,6 +36,7 @@ namespace {
 constexpr int64_t kAmbiguous = -2;
 constexpr int64_t kDead = -1;
 constexpr int kIdxWinMax = 32768;  // LDS window for candidate screening
+constexpr int kIdxCandCap = 512;   // LDS list of screened candidates (u32 window offsets)
 
 __device__ __forceinline__ uint32_t be32_global(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
@@ -151,18 +152,55 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
         hi = max(hi, xx);
     };
     if (use_lds) {
-        // 4 consecutive candidates per lane: two dword reads cover the 7
-        // bytes of their four big-endian length words
+        // Screen, then chase: 4 consecutive candidates per lane (two dword
+        // reads cover the 7 bytes of their four big-endian length words); the
+        // plausible ones go to an LDS list (wave prefix sum of per-lane
+        // counts), and the list is chased 64 candidates at a time -- one
+        // chase loop per 64 plausible positions instead of one per screening
+        // step that holds any (large blocks: 1,027 steps per chunk window).
         const lds8* wq = (const lds8*)to_lds(win) + win_off;
-        for (int64_t c0 = cb0 + 4 * lane; c0 < cend; c0 += 4 * kWave) {
+        lds32* list = (lds32*)(to_lds(win) + x.win_lds);
+        int nl = 0;  // wave-uniform list length
+        auto plausible = [&](int64_t c, uint32_t len) {
+            return c < cend && c + 4 <= Cb && len != 0 && len <= maxlen && c + 4 + (int64_t)len <= Cb;
+        };
+        auto chase_list = [&]() {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int i = lane; i < nl; i += kWave) {
+                const int r = (int)list[i];
+                const uint32_t len = __builtin_bswap32(lds_rd32(wq, r));
+                const int64_t xx = chase(in, cb0 + r + 4 + len, ce, Cb, maxlen);
+                if (xx != kDead) {
+                    lo = min(lo, xx);
+                    hi = max(hi, xx);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            nl = 0;
+        };
+        for (int64_t c0 = cb0 + 4 * lane; __builtin_amdgcn_readfirstlane((int)(c0 - 4 * lane < cend)); c0 += 4 * kWave) {
             const int r = (int)(c0 - cb0);
             const uint32_t a = lds_rd32(wq, r), b = lds_rd32(wq, r + 4);
+            uint32_t pm = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const uint32_t le = __builtin_amdgcn_alignbyte(b, a, (uint32_t)k);
-                try_cand(c0 + k, __builtin_bswap32(le));
+                pm |= plausible(c0 + k, __builtin_bswap32(le)) ? 1u << k : 0u;
             }
+            const int cnt = __builtin_popcount(pm);
+            const int incl = wave_incl_sum(cnt, lane);
+            const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+            if (total == 0) continue;
+            if (nl + total > kIdxCandCap) chase_list();
+            int at = nl + incl - cnt;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (pm & (1u << k)) list[at++] = (uint32_t)(r + k);
+            nl += total;
         }
+        chase_list();
     } else {
         // window larger than the LDS budget (large blocks): the same 4
         // candidates per lane from three absolute-aligned global dwords (an
@@ -1404,7 +1442,7 @@ hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, cons
     if (e != hipSuccess || nch == 0) return e;
     {
         ProfScope prof("k_idx_exits", s);
-        const size_t lds = (size_t)x.win_lds;
+        const size_t lds = (size_t)x.win_lds + sizeof(uint32_t) * kIdxCandCap;
         if (lds > 65536) {
             e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_idx_exits),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

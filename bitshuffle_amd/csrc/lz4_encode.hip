@@ -1778,15 +1778,23 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
     if constexpr (!WIDE && (VAR & ~256) == 0) {
         // default (byU16, every element size, single stream and batch): the
         // hand-scheduled re-test chain with its offset-2 shortcut (8192 |
-        // 32768).  A/B variants: 65536 the compiled re-test (round 3's
-        // default), 8192 the chain without the shortcut, 16384 / 24576 the
-        // hand-scheduled search windows (alone / with the chain).
+        // 32768), and for E = 1, 2, 4, 8 the hand-scheduled search windows
+        // (| 16384).  A/B variants: 65536 the compiled re-test (round 3's
+        // default), 8192 the chain without the shortcut, 16384 / 24576 /
+        // 57344 the hand-scheduled search windows (alone / with the chain /
+        // with the chain and its shortcut).
         const int v = tuning_variant();
         if (v == 65536) return launch_enc_t<EK, WIDE, VAR | 65536>(a, nb, lds, s);
         if (v == 8192) return launch_enc_t<EK, WIDE, VAR | 8192>(a, nb, lds, s);
         if (v == 16384) return launch_enc_t<EK, WIDE, VAR | 16384>(a, nb, lds, s);
         if (v == 24576) return launch_enc_t<EK, WIDE, VAR | 24576>(a, nb, lds, s);
-        if (v == 0 || v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
+        // the hand-scheduled search windows as well for the element sizes of
+        // the BASELINE configs (2 GiB G1 int16 0.716 -> 0.693 ms, 1 GiB G2
+        // float32 0.933 -> 0.914 ms per launch); odd element sizes without
+        // them (E = 3 / 12: +0.2 % / +0.8 % with them, profiles/r04/asm_search)
+        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 40960 : 57344)>(a, nb, lds, s);
+        if (v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
+        if (v == 57344) return launch_enc_t<EK, WIDE, VAR | 57344>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
