@@ -196,18 +196,25 @@ __device__ __forceinline__ void untranspose4_rows(uint32_t (&x)[8 * EK]) {
     }
 }
 
-// output byte o = (8k + i) * EK + b  <-  x[8b + i] byte k
+// output byte o = (8k + i) * EK + b  <-  x[8b + i] byte k: three v_perm_b32
+// per word (two gather two bytes each, one joins them); w is a compile-time
+// constant in every caller, so the selectors fold
 template <int EK>
 __device__ __forceinline__ uint32_t untranspose4_word(const uint32_t (&x)[8 * EK], const int w) {
-    uint32_t v = 0;
+    int r[4], k[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const int o = 4 * w + t;
         const int b = o % EK, e = o / EK;
-        const int k = e >> 3, i = e & 7;
-        v |= ((x[8 * b + i] >> (8 * k)) & 0xFFu) << (8 * t);
+        k[t] = e >> 3;
+        r[t] = 8 * b + (e & 7);
     }
-    return v;
+    // perm(S0, S1, sel): selector byte 0-3 takes S1's byte, 4-7 S0's, 12 a zero
+    const uint32_t lo = __builtin_amdgcn_perm(x[r[1]], x[r[0]],
+                                              (uint32_t)k[0] | ((uint32_t)(4 + k[1]) << 8) | 0x0C0C0000u);
+    const uint32_t hi = __builtin_amdgcn_perm(x[r[3]], x[r[2]],
+                                              (uint32_t)k[2] | ((uint32_t)(4 + k[3]) << 8) | 0x0C0C0000u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
 template <int EK>
@@ -232,12 +239,11 @@ __device__ __forceinline__ void load_group(const uint8_t* p, uint32_t (&w)[2 * E
 template <int EK>
 __device__ __forceinline__ void store_group(uint8_t* p, const uint32_t (&w)[2 * EK]) {
     if constexpr (EK == 1) {
-        *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+        *(gbl64*)p = u32x2{w[0], w[1]};
     } else {
 #pragma unroll
         for (int i = 0; i < EK / 2; i++)
-            *reinterpret_cast<uint4*>(p + 16 * i) =
-                make_uint4(w[4 * i + 0], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+            *(gbl128*)(p + 16 * i) = u32x4{w[4 * i + 0], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
     }
 }
 

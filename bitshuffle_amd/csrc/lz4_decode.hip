@@ -997,7 +997,7 @@ __device__ __forceinline__ uint32_t land_record(const PayRegsT<IT>& R, bool in_r
 // the completion of the previous block's stores (gfx9 counts loads and stores
 // on one in-order vmcnt) stalls the wave.
 template <int EK, int VAR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 4 || EK == 0 ? 4 : 5) : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 0 ? 4 : 5) : 1)))
 void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;
@@ -1132,11 +1132,13 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
 #pragma unroll
                     for (int r = 0; r < 8 * EK; r++) x[r] = D32[r * P4 + q];
                     untranspose4_rows<EK>(x);
-                    uint4* o4 = reinterpret_cast<uint4*>(dst + (int64_t)q * 32 * EK);
+                    // global (not flat) stores: a flat store also counts in
+                    // lgkmcnt, so the next LDS wait would wait for it too
+                    gbl128* o4 = (gbl128*)(dst + (int64_t)q * 32 * EK);
 #pragma unroll
                     for (int v = 0; v < 2 * EK; v++)
-                        o4[v] = make_uint4(untranspose4_word<EK>(x, 4 * v), untranspose4_word<EK>(x, 4 * v + 1),
-                                           untranspose4_word<EK>(x, 4 * v + 2), untranspose4_word<EK>(x, 4 * v + 3));
+                        o4[v] = u32x4{untranspose4_word<EK>(x, 4 * v), untranspose4_word<EK>(x, 4 * v + 1),
+                                      untranspose4_word<EK>(x, 4 * v + 2), untranspose4_word<EK>(x, 4 * v + 3)};
                 }
                 for (int g = (P4 ? P : lane); g < P; g += kWave) {
                     uint32_t w[2 * EK];
