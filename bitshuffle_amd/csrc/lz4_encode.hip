@@ -1276,6 +1276,39 @@ __device__ __forceinline__ void transpose4_regs_to_lds(const BlockRegs4<EK>& R, 
     }
 }
 
+// The same, bit-sliced over the lane's four groups at once (A/B variant bit
+// 262144): x[8b + i] gathers byte b of element i of all four groups (byte k =
+// group k, three v_perm_b32), one 8x8 bit transpose per byte lane across those
+// eight registers (untranspose4_rows: the transpose is its own inverse) leaves
+// x[8b + j] = plane 8b + j of the four groups -- ONE dword per plane as above.
+template <int EK>
+__device__ __forceinline__ void transpose4s_regs_to_lds(const BlockRegs4<EK>& R, lds8* D, int P,
+                                                        int lane) {
+    const int P4 = P >> 2;
+    lds32* D32 = (lds32*)D;
+#pragma unroll
+    for (int it = 0; it < BlockRegs4<EK>::kIters; it++) {
+        const int q = it * kWave + lane;
+        if (q < P4) {
+            uint32_t x[8 * EK];
+#pragma unroll
+            for (int b = 0; b < EK; b++) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int o = i * EK + b, d = o >> 2;
+                    const uint32_t sel = (uint32_t)(o & 3) | ((uint32_t)(4 + (o & 3)) << 8) | 0x0C0C0000u;
+                    const uint32_t lo = __builtin_amdgcn_perm(R.w[it][1][d], R.w[it][0][d], sel);
+                    const uint32_t hi = __builtin_amdgcn_perm(R.w[it][3][d], R.w[it][2][d], sel);
+                    x[8 * b + i] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+                }
+            }
+            untranspose4_rows<EK>(x);
+#pragma unroll
+            for (int r = 0; r < 8 * EK; r++) D32[r * P4 + q] = x[r];
+        }
+    }
+}
+
 // Any element size (EK == 0): the block's raw bytes (<= kRawBytes) travel
 // from HBM as coalesced 8-byte loads into registers (prefetched like the
 // EK-specialised paths), land in the still-unused hash-table LDS, and the
@@ -1414,7 +1447,10 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if (staged) {
         } else if constexpr (EK != 0) {
             if (fits4(m)) {
-                transpose4_regs_to_lds<EK>(R4, D, P, lane);
+                if constexpr ((VAR & 262144) != 0)
+                    transpose4s_regs_to_lds<EK>(R4, D, P, lane);
+                else
+                    transpose4_regs_to_lds<EK>(R4, D, P, lane);
             } else if (fits(m)) {
                 transpose_regs_to_lds<EK>(R, D, P, 0, lane);
             } else {
@@ -1779,7 +1815,7 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         // default (byU16, every element size, single stream and batch): the
         // hand-scheduled re-test chain with its offset-2 shortcut (8192 |
         // 32768), and for E = 1, 2, 4, 8 the hand-scheduled search windows
-        // (| 16384).  A/B variants: 65536 the compiled re-test (round 3's
+        // (| 16384) and the bit-sliced forward transpose (| 262144).  A/B variants: 65536 the compiled re-test (round 3's
         // default), 8192 the chain without the shortcut, 16384 / 24576 /
         // 57344 the hand-scheduled search windows (alone / with the chain /
         // with the chain and its shortcut).
@@ -1790,11 +1826,14 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 24576) return launch_enc_t<EK, WIDE, VAR | 24576>(a, nb, lds, s);
         // the hand-scheduled search windows as well for the element sizes of
         // the BASELINE configs (2 GiB G1 int16 0.716 -> 0.693 ms, 1 GiB G2
-        // float32 0.933 -> 0.914 ms per launch); odd element sizes without
-        // them (E = 3 / 12: +0.2 % / +0.8 % with them, profiles/r04/asm_search)
-        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 40960 : 57344)>(a, nb, lds, s);
+        // float32 0.933 -> 0.914 ms per launch; odd element sizes without
+        // them: E = 3 / 12 +0.2 % / +0.8 % with them, profiles/r04/asm_search),
+        // and their bit-sliced forward transpose (0.694 -> 0.676 / 0.912 ->
+        // 0.905 ms, profiles/r04/etr_sliced)
+        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 40960 : 319488)>(a, nb, lds, s);
         if (v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
         if (v == 57344) return launch_enc_t<EK, WIDE, VAR | 57344>(a, nb, lds, s);
+        if (v == 319488 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 319488>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);
