@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of whole library builds: ROUNDS x (each lib in its own fresh process),
-# G1 and G2.  Usage: bash tools/ab_libs.sh TAG GiB ROUNDS lib1.so lib2.so ...
+# G1 and G2 (GENS="1 2"; AB_ELEM=E reads them as E-byte elements).
+# Usage: bash tools/ab_libs.sh TAG GiB ROUNDS lib1.so lib2.so ...
 set -o pipefail
 TAG=$1; GIB=$2; ROUNDS=$3; shift 3
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
@@ -8,7 +9,7 @@ mkdir -p gpurun_out
 out=gpurun_out/${TAG}_ab.jsonl
 : > $out
 for r in $(seq $ROUNDS); do
-  for gen in 1 2; do
+  for gen in ${GENS:-1 2}; do
     for L in "$@"; do
       BSHUF_LIB=$PWD/$L timeout -k 10 200 python -u tools/ab_one.py $GIB $gen 3 | sed "s/^/{\"gen\": $gen, \"r\": $r, \"d\": /; s/$/}/" >> $out || exit 1
     done

@@ -20,16 +20,22 @@ dt = torch.int16 if gen == 1 else torch.float32
 n = int(gib * (1 << 30)) // (2 if gen == 1 else 4)
 x = torch.empty(n, dtype=dt, device="cuda")
 B.synth_fill_dev(x, gen)
-c = api.compress_lz4_dev(x)
-y = api.decompress_lz4_dev(c, x.shape, x.dtype)
+# AB_ELEM=E: the same bytes as E-byte elements (odd element sizes)
+es = int(os.environ.get("AB_ELEM", "0"))
+if es:
+    x = x.view(torch.uint8)[: (x.numel() * x.element_size() // es) * es]
+kw = {"elem_size": es} if es else {}
+shape = (x.numel() // es,) if es else x.shape
+c = api.compress_lz4_dev(x, **kw)
+y = api.decompress_lz4_dev(c, shape, x.dtype, **kw)
 torch.cuda.synchronize()
-assert torch.equal(x, y)
+assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
 h = hashlib.sha256(c.cpu().numpy().tobytes()).hexdigest()[:16]
 B.lib.bshuf_prof_enable(1)
 bench.prof_collect(B.lib)
 for _ in range(reps):
-    c = api.compress_lz4_dev(x)
-    y = api.decompress_lz4_dev(c, x.shape, x.dtype)
+    c = api.compress_lz4_dev(x, **kw)
+    y = api.decompress_lz4_dev(c, shape, x.dtype, **kw)
 torch.cuda.synchronize()
 k = bench.prof_collect(B.lib)
 out = {name: round(ms / cnt, 4) for name, (cnt, ms) in k.items() if ms / cnt > 0.02}
