@@ -120,6 +120,34 @@ def test_lz4_matches_oracle(bs, oracle, kind):
                 assert back.tobytes() == arr.tobytes(), (kind, E, n, block)
 
 
+def test_odd_e_deferred_copyout_alternating(bs, oracle):
+    """Odd element sizes stage each block's raw bytes at the END of the hash
+    table's LDS while the previous block's record still waits at its start
+    (deferred copy-out); an incompressible record would overlap them and is
+    flushed first.  Blocks alternate between incompressible, compressible and
+    zero bytes so both orders meet, through the host API and the default
+    blocks (8 KiB or just below)."""
+    rng = np.random.default_rng(3)
+    for E in [3, 5, 7, 12]:
+        bs_bytes = (8192 // E) // 8 * 8 * E
+        parts = []
+        for k in range(14):
+            kind = (k * 7 // 3) % 3
+            if kind == 0:
+                parts.append(rng.integers(0, 256, bs_bytes, dtype=np.uint8))
+            elif kind == 1:
+                parts.append((rng.integers(-2, 3, bs_bytes).cumsum() % 7).astype(np.uint8))
+            else:
+                parts.append(np.zeros(bs_bytes, dtype=np.uint8))
+        d = np.concatenate(parts + [rng.integers(0, 256, 5 * E, dtype=np.uint8)])
+        arr = view_e(d, E)
+        want = oracle.compress_lz4(arr)
+        got = bs.compress_lz4(arr)
+        assert got.tobytes() == want.tobytes(), E
+        back = bs.decompress_lz4(got, arr.shape, arr.dtype)
+        assert back.tobytes() == arr.tobytes(), E
+
+
 def _with_variant(bs, variant, fn):
     try:
         assert bs.lib.bshuf_set_variant(variant) == 0

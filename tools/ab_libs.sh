@@ -27,7 +27,8 @@ for r in rows:
         if k not in ("sha", "lib"):
             agg[(r["gen"], d["lib"], k)].append(v)
 for (g, lib, k), v in sorted(agg.items()):
-    if k in ("k_lz4_encode", "k_lz4_decode", "k_seq_scan", "k_compact", "k_emit"):
+    if k in ("k_lz4_encode", "k_lz4_decode", "k_seq_scan", "k_compact", "k_emit",
+             "k_seq_scan_big", "k_lz4_exec_big", "k_lz4_encode_big"):
         print("gen %d %-12s %-14s %8.3f ms  %s" % (g, lib, k, sum(v) / len(v), " ".join("%.3f" % x for x in v)))
 for g, s in shas.items():
     print("gen %d stream digests %s" % (g, "IDENTICAL" if len(s) == 1 else "DIFFER: %s" % s))

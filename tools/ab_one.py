@@ -25,6 +25,9 @@ es = int(os.environ.get("AB_ELEM", "0"))
 if es:
     x = x.view(torch.uint8)[: (x.numel() * x.element_size() // es) * es]
 kw = {"elem_size": es} if es else {}
+# AB_BS=elements: explicit block size (e.g. 131072 for 256 KiB int16 blocks)
+if int(os.environ.get("AB_BS", "0")):
+    kw["block_size"] = int(os.environ["AB_BS"])
 shape = (x.numel() // es,) if es else x.shape
 c = api.compress_lz4_dev(x, **kw)
 y = api.decompress_lz4_dev(c, shape, x.dtype, **kw)
