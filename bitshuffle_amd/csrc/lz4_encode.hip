@@ -1315,7 +1315,11 @@ __device__ __forceinline__ void transpose4s_regs_to_lds(const BlockRegs4<EK>& R,
 // bit transpose gathers each 8-element group's byte b from there -- the
 // strided byte gathers hit LDS instead of HBM.
 constexpr int kRawBytes = 8192;
+#ifndef BSHUF_EK0_DEFER
+#define BSHUF_EK0_DEFER 1
+#endif
 constexpr int kRawIters = kRawBytes / (8 * kWave);
+constexpr int kRawItems = kRawBytes / 8 / kWave;  // (group, byte) items per lane
 struct RawRegs {
     uint2 w[kRawIters];
 };
@@ -1389,9 +1393,9 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if (raw_fits(m0)) issue_raw_loads(RW, blk_src(blk), m0 * E, lane);
     }
 
-    // Deferred copy-out (EK != 0; A/B variant 4096 turns it off): a block's
-    // record stays in the table's LDS until the next block is transposed.
-    constexpr bool kDefer = EK != 0 && (VAR & 4096) == 0;
+    // Deferred copy-out (A/B variant 4096 turns it off): a block's record
+    // stays in the table's LDS until the next block is transposed.
+    constexpr bool kDefer = (EK != 0 || BSHUF_EK0_DEFER) && (VAR & 4096) == 0;
     int64_t pend_blk = -1;
     int pend_c = 0;
     auto flush_pending = [&]() {
@@ -1415,21 +1419,50 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
         if constexpr (EK == 0) {
             if (raw_fits(m)) {
                 staged = true;
-                raw_to_lds(RW, L0, n, lane);
+                // deferred copy-out: the raw bytes go to the END of the table,
+                // behind the previous block's record (flushed first when the
+                // two would overlap -- an incompressible record)
+                int rawoff = 0;
+                if constexpr (kDefer) {
+                    rawoff = (kTableBytes - ((n + 7) & ~7)) & ~15;
+                    if (pend_blk >= 0 && 16 * ((4 + pend_c + 15) >> 4) > rawoff) {
+                        flush_pending();
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+                lds8* const RS = L0 + rawoff;
+                raw_to_lds(RW, RS, n, lane);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 // lane = (group g, byte b) with b fastest: the 8 gathers of
-                // neighbouring lanes hit neighbouring bytes (no bank conflicts)
+                // neighbouring lanes hit neighbouring bytes (no bank conflicts).
+                // All of a lane's (<= 16) items are gathered before any is
+                // written, so the gathers overlap instead of each item
+                // waiting for its own
                 const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)E - 1) / (uint64_t)E);
-                for (int i = lane; i < P * E; i += kWave) {
-                    const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
-                    const lds8* x = L0 + 8 * g * E + b;
-                    uint64_t v = 0;
+                const int items = P * E;
+                uint64_t v[kRawItems];
 #pragma unroll
-                    for (int k = 0; k < 8; k++) v |= (uint64_t)x[k * E] << (8 * k);
-                    v = tr8x8(v);
+                for (int r = 0; r < kRawItems; r++) {
+                    const int i = lane + kWave * r;
+                    v[r] = 0;
+                    if (i < items) {
+                        const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                        const lds8* x = RS + 8 * g * E + b;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(v >> (8 * j));
+                        for (int k = 0; k < 8; k++) v[r] |= (uint64_t)x[k * E] << (8 * k);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < kRawItems; r++) {
+                    const int i = lane + kWave * r;
+                    if (i < items) {
+                        const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                        const uint64_t t = tr8x8(v[r]);
+#pragma unroll
+                        for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(t >> (8 * j));
+                    }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
