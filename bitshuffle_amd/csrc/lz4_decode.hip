@@ -1015,12 +1015,12 @@ __global__ __launch_bounds__(64) void k_seq_scan_big(DecArgs a, int64_t nb) {
         out.o.ph = (int)(((uintptr_t)out.o.base >> 2) & 3);
         out.o.buf = u32x4{0u, 0u, 0u, 0u};
         // the common sequence (see scan_block_lanes) straight from the LDS
-        // window while it holds the 17 bytes behind the token, else one
+        // window while it holds the 18 bytes from the token on, else one
         // scan_step (which refills the window)
         int ip = 0, op = 0, r;
         bool fast = n >= 64;
         for (;;) {
-            while (fast && (unsigned)(ip - rd.w0) <= (unsigned)(kScanWin - 17)) {
+            while (fast && (unsigned)(ip - rd.w0) <= (unsigned)(kScanWin - 18)) {
                 const int t = ip - rd.w0;
                 const int tok = (int)rd.W[t];
                 const int lit = tok >> 4, m4 = (tok & 15) + kScanMinMatch;
