@@ -813,65 +813,6 @@ struct GReader {
     __device__ __forceinline__ uint32_t operator()(int p) { return gw_byte(g, P, clen, p); }
 };
 
-// Dword d (0..7) of a lane's 32-byte window.
-__device__ __forceinline__ uint32_t gw_dword(const GWin& g, int d) {
-    const u32x4 v = d < 4 ? g.a : g.b;
-    const int e = d & 3;
-    return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-}
-
-// scan_block for one block per LANE, in two levels.  A wave whose lanes step
-// scan_step together runs, in almost every step, the union of all its paths
-// (length runs, the safe loop, the last sequence) for the few lanes that need
-// them -- the scan was VALU-bound on exactly that.  Here the common sequence
-// -- both lengths < 15, far from both ends of the block, in the fast loop --
-// is stepped by every lane that is at one, from its register window (the
-// token is in the window's first granule, the offset in the 32 bytes), until
-// no lane is; then one scan_step for every lane (each at an uncommon
-// sequence).  The common step's conditions are exactly those under which
-// scan_step's fast loop takes that sequence without a branch of its own.
-template <class Out>
-__device__ __forceinline__ int scan_block_lanes(GReader& rd, const int clen, const int n, Out& out,
-                                                int& cnt) {
-    int ip = 0, op = 0;
-    cnt = 0;
-    bool fast = n >= 64;  // FASTLOOP_SAFE_DISTANCE
-    for (;;) {
-        for (;;) {
-            bool can = false;
-            int lit = 0, m4 = 0;
-            if (fast) {
-                if ((unsigned)(ip - rd.g.w0) > 15u) {
-                    const uint8_t* ap = rd.P + ip;
-                    rd.g.w0 = ip - (int)((uintptr_t)ap & 15);
-                    const gbl128c* q = g128_aligned_down(ap);
-                    rd.g.a = q[0];
-                    if (rd.g.w0 + 16 < clen) rd.g.b = q[1];
-                }
-                const int t = ip - rd.g.w0;
-                const int e = t >> 2;
-                const uint32_t tw = e == 0 ? rd.g.a.x : (e == 1 ? rd.g.a.y : (e == 2 ? rd.g.a.z : rd.g.a.w));
-                const int tok = (int)((tw >> (8 * (t & 3))) & 255u);
-                lit = tok >> 4;
-                m4 = (tok & 15) + kScanMinMatch;
-                const int t2 = t + 1 + lit;  // <= 31: the offset's bytes are in the window when it counts
-                const int d = t2 >> 2;
-                const uint32_t w2 = __builtin_amdgcn_alignbyte(gw_dword(rd.g, min(d + 1, 7)), gw_dword(rd.g, d),
-                                                               (uint32_t)(t2 & 3));
-                can = scan_common(tok, (int)(w2 & 0xFFFFu), ip, op, clen, n);
-            }
-            if (!ballot(can)) break;
-            if (can) {
-                out.put(cnt++, (uint32_t)ip, op);
-                ip += 3 + lit;
-                op += lit + m4;
-            }
-        }
-        const int r = scan_step(rd, clen, n, out, ip, op, cnt, fast);
-        if (r != kScanCont) return r;
-    }
-}
-
 // Token positions of one lane's block, four per 16-byte store: entry i sits
 // in dword slot (ph + i) & 3 of its absolute 16-byte chunk, and a chunk is
 // stored whole once its slot 3 is filled -- unless it begins before the
@@ -922,12 +863,7 @@ struct SeqOut {
 // for an LZ4 failure, -91 when the block does not decode to exactly n bytes).
 // seq[offs[k]/3 + i] = payload position of sequence i's token (a sequence
 // takes >= 3 record bytes, so the per-block ranges are disjoint).
-#ifdef BSHUF_SCAN_WAVES
-#define BSHUF_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(BSHUF_SCAN_WAVES)))
-#else
-#define BSHUF_SCAN_ATTR
-#endif
-__global__ __launch_bounds__(256) BSHUF_SCAN_ATTR void k_seq_scan(DecArgs a, int64_t nb) {
+__global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     const int64_t k = a.blk0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= a.blk1) return;
     const BlockLoc loc = block_loc(a, k, nb, a.segs ? a.blk_seg[k] : 0u);
@@ -948,7 +884,7 @@ __global__ __launch_bounds__(256) BSHUF_SCAN_ATTR void k_seq_scan(DecArgs a, int
         out.base = loc.seq + o0 / 3;
         out.ph = (int)(((uintptr_t)out.base >> 2) & 3);
         out.buf = u32x4{0u, 0u, 0u, 0u};
-        const int r = scan_block_lanes(rd, (int)clen, n, out, cnt);
+        const int r = scan_block(rd, (int)clen, n, out, cnt);
         out.flush(cnt);  // a rejected block's positions are never read
         st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
         // valid: bits 32..47 carry max(output start - token position) + 2^14,
@@ -1014,25 +950,7 @@ __global__ __launch_bounds__(64) void k_seq_scan_big(DecArgs a, int64_t nb) {
         out.o.base = loc.seq + o0 / 3;
         out.o.ph = (int)(((uintptr_t)out.o.base >> 2) & 3);
         out.o.buf = u32x4{0u, 0u, 0u, 0u};
-        // the common sequence (see scan_block_lanes) straight from the LDS
-        // window while it holds the 18 bytes from the token on, else one
-        // scan_step (which refills the window)
-        int ip = 0, op = 0, r;
-        bool fast = n >= 64;
-        for (;;) {
-            while (fast && (unsigned)(ip - rd.w0) <= (unsigned)(kScanWin - 18)) {
-                const int t = ip - rd.w0;
-                const int tok = (int)rd.W[t];
-                const int lit = tok >> 4, m4 = (tok & 15) + kScanMinMatch;
-                const int off = (int)rd.W[t + 1 + lit] | ((int)rd.W[t + 2 + lit] << 8);
-                if (!scan_common(tok, off, ip, op, (int)clen, n)) break;
-                out.put(cnt++, (uint32_t)ip, op);
-                ip += 3 + lit;
-                op += lit + m4;
-            }
-            r = scan_step(rd, (int)clen, n, out, ip, op, cnt, fast);
-            if (r != kScanCont) break;
-        }
+        const int r = scan_block(rd, (int)clen, n, out, cnt);
         if (lane == 0) out.o.flush(cnt);
         st = r < 0 ? (int64_t)r - 1000 : (r == n ? (int64_t)cnt : -91);
     }
@@ -1078,11 +996,8 @@ __device__ __forceinline__ uint32_t land_record(const PayRegsT<IT>& R, bool in_r
 // i.  Every wait on HBM therefore follows a parse, so neither load latency nor
 // the completion of the previous block's stores (gfx9 counts loads and stores
 // on one in-order vmcnt) stalls the wave.
-#ifndef BSHUF_DEC_EK0_WAVES
-#define BSHUF_DEC_EK0_WAVES 4
-#endif
 template <int EK, int VAR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 0 ? BSHUF_DEC_EK0_WAVES : 5) : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((VAR & 512) ? (EK == 0 ? 4 : 5) : 1)))
 void k_lz4_decode(DecArgs a, int64_t nb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x;

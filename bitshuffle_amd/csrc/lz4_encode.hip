@@ -1319,7 +1319,6 @@ constexpr int kRawBytes = 8192;
 #define BSHUF_EK0_DEFER 1
 #endif
 constexpr int kRawIters = kRawBytes / (8 * kWave);
-constexpr int kRawItems = kRawBytes / 8 / kWave;  // (group, byte) items per lane
 struct RawRegs {
     uint2 w[kRawIters];
 };
@@ -1436,33 +1435,17 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 // lane = (group g, byte b) with b fastest: the 8 gathers of
-                // neighbouring lanes hit neighbouring bytes (no bank conflicts).
-                // All of a lane's (<= 16) items are gathered before any is
-                // written, so the gathers overlap instead of each item
-                // waiting for its own
+                // neighbouring lanes hit neighbouring bytes (no bank conflicts)
                 const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)E - 1) / (uint64_t)E);
-                const int items = P * E;
-                uint64_t v[kRawItems];
+                for (int i = lane; i < P * E; i += kWave) {
+                    const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
+                    const lds8* x = RS + 8 * g * E + b;
+                    uint64_t v = 0;
 #pragma unroll
-                for (int r = 0; r < kRawItems; r++) {
-                    const int i = lane + kWave * r;
-                    v[r] = 0;
-                    if (i < items) {
-                        const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
-                        const lds8* x = RS + 8 * g * E + b;
+                    for (int k = 0; k < 8; k++) v |= (uint64_t)x[k * E] << (8 * k);
+                    v = tr8x8(v);
 #pragma unroll
-                        for (int k = 0; k < 8; k++) v[r] |= (uint64_t)x[k * E] << (8 * k);
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < kRawItems; r++) {
-                    const int i = lane + kWave * r;
-                    if (i < items) {
-                        const int g = (int)__umulhi((uint32_t)i, magic), b = i - g * E;
-                        const uint64_t t = tr8x8(v[r]);
-#pragma unroll
-                        for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(t >> (8 * j));
-                    }
+                    for (int j = 0; j < 8; j++) D[(8 * b + j) * P + g] = (uint8_t)(v >> (8 * j));
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();

@@ -31,135 +31,110 @@ BSHUF_HD inline bool scan_len(Rd& rd, int& ip, int ilimit, bool initial_check, i
     return true;
 }
 
-// scan_step's "not finished" result (a finished block returns op >= 0 or
-// -(ip)-1 > INT_MIN).
-constexpr int kScanCont = -0x7FFFFFFF - 1;
-
-// One sequence of the control flow of LZ4_decompress_safe (LZ4 1.10.0,
-// lz4/lz4.c:2022-2445; restated and pinned against the compiled reference in
-// oracle/bshuf_oracle.c) without the copies: the fast loop (2083-2209) and the
-// safe loop (2215-2435) check different margins, so both are followed to
-// reach the same accept / reject decision and error position.  Advances the
-// state (ip, op, cnt, fast) past the sequence at ip and returns kScanCont, or
-// returns op (bytes the block decodes to) or -(ip)-1 when the block ends
-// there.  Each sequence's token position goes to out.put(i, pos, op) in
-// increasing i, with op the output position where that sequence starts (a
-// rejected block may have put one more).
-template <class Rd, class Out>
-BSHUF_HD inline int scan_step(Rd& rd, const int clen, const int n, Out& out, int& ip, int& op,
-                              int& cnt, bool& fast) {
-    enum { kNone, kLit, kCopyMatch, kMatch };
-    const int tp = ip;
-    const int tok = (int)rd(ip++);
-    int len = tok >> 4, ml = 0, off = 0, add = 0;
-    int entry = kNone;
-    if (fast) {
-        if (len == 15) {
-            if (!scan_len(rd, ip, clen - 15, true, add)) return -ip - 1;
-            len += add;
-            if (op + len > n - 32 || ip + len > clen - 32) entry = kLit;
-        } else if (ip > clen - 17) {
-            entry = kLit;
-        }
-        if (entry == kNone) {
-            out.put(cnt++, (uint32_t)tp, op);
-            ip += len;
-            op += len;
-            off = (int)(rd(ip) | (rd(ip + 1) << 8));
-            ip += 2;
-            ml = tok & 15;
-            if (ml == 15) {
-                if (!scan_len(rd, ip, clen - 4, false, add)) return -ip - 1;
-                ml += add + kScanMinMatch;
-                if (op + ml >= n - 64) entry = kMatch;
-            } else {
-                ml += kScanMinMatch;
-                if (op + ml >= n - 64) {
-                    entry = kMatch;
-                } else if (off >= 8 && off <= op) {
-                    op += ml;
-                    return kScanCont;
-                }
-            }
-            if (entry == kNone) {
-                if (off > op) return -ip - 1;
-                op += ml;
-                return kScanCont;
-            }
-        }
-        fast = false;  // the rest of the block runs in the safe loop
-    } else {
-        if (len != 15 && ip < clen - 16 && op <= n - 32) {
-            out.put(cnt++, (uint32_t)tp, op);
-            ip += len;
-            op += len;
-            ml = tok & 15;
-            off = (int)(rd(ip) | (rd(ip + 1) << 8));
-            ip += 2;
-            if (ml != 15 && off >= 8 && off <= op) {
-                op += ml + kScanMinMatch;
-                return kScanCont;
-            }
-            entry = kCopyMatch;
-        } else {
-            if (len == 15) {
-                if (!scan_len(rd, ip, clen - 15, true, add)) return -ip - 1;
-                len += add;
-            }
-            entry = kLit;
-        }
-    }
-    if (entry == kLit) {
-        out.put(cnt++, (uint32_t)tp, op);
-        const int cpy = op + len;
-        if (cpy > n - 12 || ip + len > clen - 8) {
-            // must be the last sequence: consume the input exactly
-            if (ip + len != clen || cpy > n) {
-                cnt--;
-                return -ip - 1;
-            }
-            return cpy;
-        }
-        ip += len;
-        op = cpy;
-        off = (int)(rd(ip) | (rd(ip + 1) << 8));
-        ip += 2;
-        ml = tok & 15;
-        entry = kCopyMatch;
-    }
-    if (entry == kCopyMatch) {
-        if (ml == 15) {
-            if (!scan_len(rd, ip, clen - 4, false, add)) return -ip - 1;
-            ml += add;
-        }
-        ml += kScanMinMatch;
-    }
-    // safe_match_copy
-    if (off > op) return -ip - 1;
-    if (op + ml > n - 5) return -ip - 1;  // the last LASTLITERALS bytes are literals
-    op += ml;
-    return kScanCont;
-}
-
-// The common sequence: both lengths < 15, far from both ends of the block, in
-// the fast loop -- exactly where scan_step's fast loop takes the sequence at
-// ip without a branch of its own (put, then ip += 3 + lit, op += lit + ml).
-// tok = the byte at ip, off = the two bytes behind its literals.
-BSHUF_HD inline bool scan_common(int tok, int off, int ip, int op, int clen, int n) {
-    const int lit = tok >> 4, m = tok & 15;
-    return lit < 15 && m < 15 && ip + 1 <= clen - 17 && op + lit + m + kScanMinMatch < n - 64 &&
-           off <= op + lit;
-}
-
-// The whole block: scan_step until it finishes.  Returns op or -(ip)-1.
+// The control flow of LZ4_decompress_safe (LZ4 1.10.0, lz4/lz4.c:2022-2445;
+// restated and pinned against the compiled reference in oracle/bshuf_oracle.c)
+// without the copies: the fast loop (2083-2209) and the safe loop (2215-2435)
+// check different margins, so both are followed to reach the same accept /
+// reject decision and error position.  Records each sequence's token position.
+// Returns op (bytes the block decodes to) or -(ip)-1.  Token positions go to
+// out.put(i, pos, op) in increasing i, with op the output position where that
+// sequence starts (a rejected block may have put one more).
 template <class Rd, class Out>
 BSHUF_HD inline int scan_block(Rd& rd, const int clen, const int n, Out& out, int& cnt) {
+    enum { kNone, kLit, kCopyMatch, kMatch };
     int ip = 0, op = 0;
     cnt = 0;
     bool fast = n >= 64;  // FASTLOOP_SAFE_DISTANCE
     for (;;) {
-        const int r = scan_step(rd, clen, n, out, ip, op, cnt, fast);
-        if (r != kScanCont) return r;
+        const int tp = ip;
+        const int tok = (int)rd(ip++);
+        int len = tok >> 4, ml = 0, off = 0, add = 0;
+        int entry = kNone;
+        if (fast) {
+            if (len == 15) {
+                if (!scan_len(rd, ip, clen - 15, true, add)) return -ip - 1;
+                len += add;
+                if (op + len > n - 32 || ip + len > clen - 32) entry = kLit;
+            } else if (ip > clen - 17) {
+                entry = kLit;
+            }
+            if (entry == kNone) {
+                out.put(cnt++, (uint32_t)tp, op);
+                ip += len;
+                op += len;
+                off = (int)(rd(ip) | (rd(ip + 1) << 8));
+                ip += 2;
+                ml = tok & 15;
+                if (ml == 15) {
+                    if (!scan_len(rd, ip, clen - 4, false, add)) return -ip - 1;
+                    ml += add + kScanMinMatch;
+                    if (op + ml >= n - 64) entry = kMatch;
+                } else {
+                    ml += kScanMinMatch;
+                    if (op + ml >= n - 64) {
+                        entry = kMatch;
+                    } else if (off >= 8 && off <= op) {
+                        op += ml;
+                        continue;
+                    }
+                }
+                if (entry == kNone) {
+                    if (off > op) return -ip - 1;
+                    op += ml;
+                    continue;
+                }
+            }
+            fast = false;  // the rest of the block runs in the safe loop
+        } else {
+            if (len != 15 && ip < clen - 16 && op <= n - 32) {
+                out.put(cnt++, (uint32_t)tp, op);
+                ip += len;
+                op += len;
+                ml = tok & 15;
+                off = (int)(rd(ip) | (rd(ip + 1) << 8));
+                ip += 2;
+                if (ml != 15 && off >= 8 && off <= op) {
+                    op += ml + kScanMinMatch;
+                    continue;
+                }
+                entry = kCopyMatch;
+            } else {
+                if (len == 15) {
+                    if (!scan_len(rd, ip, clen - 15, true, add)) return -ip - 1;
+                    len += add;
+                }
+                entry = kLit;
+            }
+        }
+        if (entry == kLit) {
+            out.put(cnt++, (uint32_t)tp, op);
+            const int cpy = op + len;
+            if (cpy > n - 12 || ip + len > clen - 8) {
+                // must be the last sequence: consume the input exactly
+                if (ip + len != clen || cpy > n) {
+                    cnt--;
+                    return -ip - 1;
+                }
+                return cpy;
+            }
+            ip += len;
+            op = cpy;
+            off = (int)(rd(ip) | (rd(ip + 1) << 8));
+            ip += 2;
+            ml = tok & 15;
+            entry = kCopyMatch;
+        }
+        if (entry == kCopyMatch) {
+            if (ml == 15) {
+                if (!scan_len(rd, ip, clen - 4, false, add)) return -ip - 1;
+                ml += add;
+            }
+            ml += kScanMinMatch;
+        }
+        // safe_match_copy
+        if (off > op) return -ip - 1;
+        if (op + ml > n - 5) return -ip - 1;  // the last LASTLITERALS bytes are literals
+        op += ml;
     }
 }
 

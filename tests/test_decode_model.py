@@ -20,17 +20,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOSTCHECK = os.path.join(ROOT, "bitshuffle_amd", "libbshuf_hostcheck.so")
 
 
-# scan: the state machine one sequence at a time (scan_block); scan2: the
-# two-level form the device token scans run (common sequences by scan_common,
-# the rest by scan_step)
-@pytest.fixture(scope="module", params=["bshuf_hostcheck_scan", "bshuf_hostcheck_scan2"])
-def scan(request):
+@pytest.fixture(scope="module")
+def scan():
     if not os.path.exists(HOSTCHECK):
         import subprocess
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "bitshuffle_amd"),
                                HOSTCHECK])
     lib = ctypes.CDLL(HOSTCHECK)
-    fn = getattr(lib, request.param)
+    fn = lib.bshuf_hostcheck_scan
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                    ctypes.POINTER(ctypes.c_int)]
@@ -90,31 +87,3 @@ def test_scan_matches_oracle_on_corrupt_blocks(oracle, scan):
                 accepted += 1
         checked += 1
     assert checked > 1000 and accepted > 50
-
-
-def test_two_level_scan_equals_scan(oracle):
-    """The two-level scan puts exactly scan_block's token positions and returns
-    its result, on valid and corrupt blocks."""
-    lib = ctypes.CDLL(HOSTCHECK)
-    fns = [lib.bshuf_hostcheck_scan, lib.bshuf_hostcheck_scan2]
-    for fn in fns:
-        fn.restype = ctypes.c_int
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                       ctypes.POINTER(ctypes.c_int)]
-
-    def both(comp, n):
-        comp = np.ascontiguousarray(comp, dtype=np.uint8)
-        res = []
-        for fn in fns:
-            pos = np.zeros(comp.size // 3 + 2, dtype=np.uint32)
-            cnt = ctypes.c_int(0)
-            r = fn(comp.ctypes.data, comp.size, n, pos.ctypes.data, ctypes.byref(cnt))
-            res.append((r, pos[:max(cnt.value, 0)].tobytes()))
-        return res
-    cases = [(oracle.lz4_compress_block(d), d.size) for d in _blocks(oracle)]
-    cases += [(c, cap) for c, cap in corrupt_lz4_blocks(oracle, seed=7, per_base=25) if cap]
-    for comp, n in cases:
-        a, b = both(comp, n)
-        assert a[0] == b[0], (comp.size, n, a[0], b[0])
-        if a[0] >= 0:
-            assert a[1] == b[1], (comp.size, n)
