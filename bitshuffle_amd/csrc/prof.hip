@@ -203,6 +203,18 @@ void bshuf_prof_enable(int on) {
     Prof& p = P();
     std::lock_guard<std::mutex> g(p.mu);
     p.on = on != 0;
+    // events made here, not per launch: hipEventCreate costs tens of us of
+    // host time, which a timed region where the host is behind the GPU (after
+    // a compress's result is read back) would otherwise pay per kernel
+    // (measured: ~0.3 ms of GPU idle per config-2 step, r4f2 kernel trace)
+    if (p.on) {
+        const size_t want = 4096 + p.recs.size() * 2;
+        while (p.pool.size() < want) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            p.pool.push_back(e);
+        }
+    }
 }
 
 // Writes "name count total_ms\n" lines into buf; returns the number of bytes
