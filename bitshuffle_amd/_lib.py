@@ -41,6 +41,7 @@ PROTOTYPES = {
     "bshuf_decompress_lz4_batch_dev": (_i64, [_vp, _vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp]),
     "bshuf_synth_fill_dev": (_i64, [_vp, _sz, _int, _u64, _u64, _vp]),
     "bshuf_prof_enable": (None, [_int]),
+    "bshuf_prof_only": (None, [ctypes.c_char_p]),
     "bshuf_set_variant": (_int, [_int]),
     "bshuf_prof_collect": (_sz, [ctypes.c_char_p, _sz]),
     "bshuf_host_poison": (_i64, [_int]),

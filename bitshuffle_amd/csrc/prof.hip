@@ -32,6 +32,7 @@ struct Rec {
 struct Prof {
     std::mutex mu;
     bool on = false;
+    std::string only;  // non-empty: time only the kernel of this name
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     hipEvent_t get() {
@@ -156,6 +157,7 @@ ProfScope::ProfScope(const char* name, hipStream_t s) : name_(name), s_(s), a_(n
     Prof& p = P();
     if (!p.on) return;
     std::lock_guard<std::mutex> g(p.mu);
+    if (!p.only.empty() && p.only != name) return;
     a_ = p.get();
     (void)hipEventRecord((hipEvent_t)a_, s);
 }
@@ -215,6 +217,16 @@ void bshuf_prof_enable(int on) {
             p.pool.push_back(e);
         }
     }
+}
+
+// Restricts the timing to one kernel name (NULL or "": every kernel).  Each
+// timed launch adds two event records to its stream (~0.2 ms per config-2
+// step when every kernel is timed: bench.py times them all in its warmup and
+// only the dominant kernel in its timed region).
+void bshuf_prof_only(const char* name) {
+    Prof& p = P();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.only = name ? name : "";
 }
 
 // Writes "name count total_ms\n" lines into buf; returns the number of bytes

@@ -100,6 +100,8 @@ int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first,
  * benchmarks: enable, run, then collect "name count total_ms" lines.
  * bshuf_prof_collect returns the buffer size needed and resets. */
 void bshuf_prof_enable(int on);
+/* Times only the kernel of this name (NULL: every kernel). */
+void bshuf_prof_only(const char* name);
 /* Selects, for the CALLING THREAD only, an alternative kernel variant for A/B
  * measurements: 0 default, 2 inline LZ4 emitter, 4 one-group-per-lane
  * transpose, 8 re-test table lookup by lane 0's returning exchange, decoder
