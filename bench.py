@@ -8,8 +8,10 @@ buffer (fused transpose + LZ4 kernel, offset scan, compaction) +
 bshuf_decompress_lz4_dev of the framed stream it produced (parallel
 block-index rebuild from the framing -- the encoder's offsets are NOT reused --
 then fused LZ4 decode + inverse transpose).  Inputs are generated on the
-device before timing; nothing crosses PCIe inside the timed region except the
-8-byte compressed length the decoder needs.
+device before timing; nothing crosses PCIe inside the timed region: the
+decoder reads the stream length from the encoder's device result word
+(bshuf_decompress_lz4_dev_dlen / _batch_dev_dlen), so a step never waits on
+the host between the two calls.
 
 The other BASELINE configs (parity-tested separately, not the headline line):
   --config 1  bshuf_bitshuffle + bshuf_bitunshuffle of the 64 MiB int32 ramp
@@ -42,6 +44,13 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident GiB/s bitshuffle+LZ4 encode+decode, 4 GiB int16; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
+
+# kernels the library ran on the pipelined encode's side stream (launch.h
+# kPipeSegs; their profiling names end in "_side"): they run beside the parse,
+# so their event times overlap the step's other kernels
+def overlapped(name):
+    return name.endswith("_side")
+
 
 CONFIGS = {
     1: dict(gen=0, dtype="int32", gib=1.0 / 16, what="shuffle"),
@@ -210,10 +219,22 @@ def copy_peak_gbps(dev, nbytes=2 << 30, reps=5):
 # ------------------------------------------------------------ parity digests
 def load_digests():
     """SHA-256 digests of the REFERENCE's own output at full BASELINE sizes
-    (tests/golden/vectors.json "full", made by tests/golden/make_vectors.py
-    from oracle/_ref, the reference C compiled from /root/reference)."""
+    and for the element-size / block-size modes (tests/golden/vectors.json
+    "full" and "modes", made by tests/golden/make_vectors.py from oracle/_ref,
+    the reference C compiled from /root/reference)."""
     p = os.path.join(ROOT, "tests", "golden", "vectors.json")
-    return {v["name"]: v for v in json.load(open(p))["full"]}
+    v = json.load(open(p))
+    return {e["name"]: e for e in v["full"] + v.get("modes", [])}
+
+
+def mode_digest(digests, gen, E, bsz, nbytes):
+    """The reference digest of a --elem-size / --block-size line's exact input
+    (G1 int16 bytes, seed 12345, first nbytes framed as E-byte elements)."""
+    for d in digests.values():
+        if (d["name"].startswith("mode_") and gen == 1 and d["elem_size"] == E
+                and d["bs"] == bsz and d["nbytes"] == nbytes):
+            return d
+    return None
 
 
 def sha256_dev(t, nbytes=None):
@@ -387,16 +408,24 @@ def main(argv=None):
         ys = [torch.empty_like(x) for x in xs]
         state = {}
 
+        shapes = [x.shape for x in xs]
+
         def step():
+            # stream lengths stay on the device: the decoder reads them there
             _, res = api.compress_lz4_batch_dev(xs, outs=outs, sync=False)
-            counts = res.cpu().tolist()  # the decoder needs the stream lengths
-            state["C"] = sum(counts)
+            state["res"] = res
+            state["dres"] = api.decompress_lz4_batch_dev(outs, shapes, dt, outs=ys, sync=False,
+                                                         lengths=res)[1]
+
+        def lengths():  # after the timed region
+            counts = state["res"].cpu().tolist()
             state["counts"] = counts
-            api.decompress_lz4_batch_dev([o[:c] for o, c in zip(outs, counts)],
-                                         [x.shape for x in xs], dt, outs=ys, sync=False)
+            state["C"] = sum(counts)
 
         def check():
-            return all(torch.equal(x, y) for x, y in zip(xs, ys))
+            lengths()
+            return (state["dres"].cpu().tolist() == state["counts"]
+                    and all(torch.equal(x, y) for x, y in zip(xs, ys)))
         workload = ("batch of %d independent %d MiB %s G1 chunks per GPU (seed 12345 + global "
                     "chunk id), default 8 KiB blocks, bshuf_*_lz4_batch_dev: one launch per kernel "
                     "for all chunks, device-resident, decoder rebuilds each chunk's block index"
@@ -413,6 +442,9 @@ def main(argv=None):
         def step():
             api.bitshuffle_dev(x, out=s_buf)
             api.bitunshuffle_dev(s_buf, out=y)
+
+        def lengths():
+            pass
 
         def check():
             return torch.equal(x, y)
@@ -435,7 +467,7 @@ def main(argv=None):
         wse = torch.empty(max(int(lib.bshuf_compress_lz4_dev_workspace(n, E, bsz)), 256),
                           dtype=torch.uint8, device=dev)
         wsd = torch.empty(max(int(lib.bshuf_decompress_lz4_dev_workspace(bound, n, E, bsz)), 256),
-                          dtype=torch.uint8, device=dev)
+                          dtype=torch.uint8, device=dev)  # capacity-sized (device-held length)
         res_e = torch.empty(1, dtype=torch.int64, device=dev)
         res_d = torch.empty(1, dtype=torch.int64, device=dev)
         y = torch.empty_like(x)
@@ -449,15 +481,18 @@ def main(argv=None):
                                            None, st)
             if r < 0:
                 raise SystemExit("bshuf_compress_lz4_dev: %d" % r)
-            c = int(res_e.item())
-            state["C"] = c
-            r = lib.bshuf_decompress_lz4_dev(vp(comp.data_ptr()), c, vp(y.data_ptr()), n, E, bsz,
-                                             vp(wsd.data_ptr()), wsd.numel(), vp(res_d.data_ptr()),
-                                             None, st)
+            # the stream length stays on the device (res_e)
+            r = lib.bshuf_decompress_lz4_dev_dlen(vp(comp.data_ptr()), vp(res_e.data_ptr()), bound,
+                                                  vp(y.data_ptr()), n, E, bsz, vp(wsd.data_ptr()),
+                                                  wsd.numel(), vp(res_d.data_ptr()), None, st)
             if r < 0:
-                raise SystemExit("bshuf_decompress_lz4_dev: %d" % r)
+                raise SystemExit("bshuf_decompress_lz4_dev_dlen: %d" % r)
+
+        def lengths():
+            state["C"] = int(res_e.item())
 
         def check():
+            lengths()
             return int(res_d.item()) == state["C"] and torch.equal(x, y)
         workload = ("bitshuffle+LZ4 encode+decode round trip, %.3g GiB of %s %s bytes per GPU read as "
                     "%d-byte elements, block size %d elements (%d bytes), device-resident, decoder "
@@ -481,12 +516,15 @@ def main(argv=None):
 
         def step():
             api.compress_lz4_dev(x, out=comp, workspace=ws_enc, result=res_e, sync=False)
-            c = int(res_e.item())  # the decoder needs the stream length on the host
-            state["C"] = c
-            api.decompress_lz4_dev(comp[:c], x.shape, x.dtype, out=y, workspace=ws_dec,
-                                   result=res_d, sync=False)
+            # the stream length stays on the device: the decoder reads res_e
+            api.decompress_lz4_dev(comp, x.shape, x.dtype, out=y, workspace=ws_dec,
+                                   result=res_d, sync=False, length=res_e)
+
+        def lengths():
+            state["C"] = int(res_e.item())
 
         def check():
+            lengths()
             return int(res_d.item()) == state["C"] and torch.equal(x, y)
         workload = ("bitshuffle+LZ4 encode+decode round trip, %.3g GiB %s %s per GPU, default "
                     "blocks (%d elem), device-resident, decoder rebuilds the block index" % (
@@ -512,6 +550,13 @@ def main(argv=None):
                   (d["name"], "compressed_len", state["C"], d["compressed_len"]),
                   (d["name"], "compressed_sha256", sha256_dev(comp, state["C"]),
                    d["compressed_sha256"])]
+    elif cfg["what"] == "lz4" and rank == 0 and (args.elem_size or args.block_size):
+        d = mode_digest(digests, cfg["gen"], es, args.block_size or 0, nbytes)
+        if d is not None:
+            pairs += [(d["name"], "input_sha256", sha256_dev(x), d["input_sha256"]),
+                      (d["name"], "compressed_len", state["C"], d["compressed_len"]),
+                      (d["name"], "compressed_sha256", sha256_dev(comp, state["C"]),
+                       d["compressed_sha256"])]
     elif cfg["what"] == "batch" and cfg["chunk_mib"] == 32:
         for i in range(nchunks):
             name = "cfg4_g1_chunk%04d" % (rank * nchunks + i)
@@ -540,7 +585,7 @@ def main(argv=None):
             torch.cuda.synchronize()
             kern_all = prof_collect(lib)
             # (the hipcub scans' event times include waiting for free LDS)
-            dom_name = max((k for k in kern_all if not k.startswith("scan_")),
+            dom_name = max((k for k in kern_all if not k.startswith("scan_") and not overlapped(k)),
                            key=lambda k: kern_all[k][1])
             lib.bshuf_prof_only(dom_name.encode())
             warm = 0
@@ -552,6 +597,7 @@ def main(argv=None):
         if not kern_all:  # no warmup: every kernel was timed in the timed steps
             kern_all = kern
     breakdown_steps = float(args.warmup if args.warmup > 0 else args.steps)
+    lengths()  # the last step's stream length(s), read back after the timed region
     C = state["C"]
     total_bytes = sum_over_ranks(float(nbytes) * args.steps, world, dev)
     value = total_bytes / elapsed / GIB
@@ -562,7 +608,8 @@ def main(argv=None):
     if kern:
         # algorithmic bytes per launch, SURVEY.md 8(d): encode N + C, decode
         # C + N, transposes 2N (scratch / index traffic is not credited)
-        alg = {"k_lz4_encode": nbytes + C, "k_lz4_decode": C + nbytes, "k_compact": C,
+        alg = {"k_lz4_encode": nbytes + C, "k_lz4_decode": C + nbytes, "k_compact": 2 * C,
+               "k_compact_side": 2 * C,
                "k_idx_exits": C, "k_seq_scan": C, "k_bitshuffle": 2 * nbytes,
                "k_bitunshuffle": 2 * nbytes}
         for name, (cnt, ms) in kern_all.items():
@@ -576,7 +623,14 @@ def main(argv=None):
         alg_launch = alg.get(dom, nbytes + C) / per_step_launches
         ach = alg_launch / avg_s / 1e9
         pmc = load_pmc_traffic()
-        traffic = pmc.get(dom) if isinstance(pmc, dict) and args.config == 2 else None
+        # only for the workload the committed PMC passes measured: same data,
+        # element size, block size and call size (else the per-launch bytes
+        # belong to another kernel configuration)
+        wl = pmc.get("_workload") if isinstance(pmc, dict) else None
+        same = (isinstance(wl, dict) and cfg["what"] == "lz4" and wl.get("gen") == cfg["gen"]
+                and wl.get("elem_size") == es and wl.get("block_size") == (args.block_size or 0)
+                and wl.get("bytes_per_call") == nbytes)
+        traffic = pmc.get(dom) if same else None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic,
@@ -626,10 +680,13 @@ def main(argv=None):
             # every kernel's event-timed launches in the warmup steps (the
             # timed steps time only the roofline's kernel); side-stream kernels
             # of the pipelined encode (k_compact, scan_block_offsets) overlap
-            # the parse, and an event-timed scan includes its wait for free LDS
+            # the parse, and an event-timed scan includes its wait for free LDS:
+            # they are listed apart and do not add to the step
             "kernels_avg_ms": kernels,
             "kernels_ms_per_step": {k: round(v[1] / breakdown_steps, 4)
-                                    for k, v in kern_all.items()},
+                                    for k, v in kern_all.items() if not overlapped(k)},
+            "kernels_ms_per_step_overlapped": {k: round(v[1] / breakdown_steps, 4)
+                                               for k, v in kern_all.items() if overlapped(k)},
             "kernels_timed_in": "warmup steps" if args.warmup > 0 else "timed steps",
             "parity": parity, "cpu_baseline": cpu, "dist": dist_info(),
         }

@@ -35,10 +35,14 @@ PROTOTYPES = {
     "bshuf_lz4_dev_nblocks": (_sz, [_sz, _sz, _sz]),
     "bshuf_compress_lz4_dev": (_i64, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp, _vp]),
     "bshuf_decompress_lz4_dev": (_i64, [_vp, _sz, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp, _vp]),
+    "bshuf_decompress_lz4_dev_dlen": (_i64, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp,
+                                             _vp]),
     "bshuf_compress_lz4_batch_dev_workspace": (_sz, [_vp, _sz, _sz, _sz]),
     "bshuf_compress_lz4_batch_dev": (_i64, [_vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp, _vp]),
     "bshuf_decompress_lz4_batch_dev_workspace": (_sz, [_vp, _vp, _sz, _sz, _sz]),
     "bshuf_decompress_lz4_batch_dev": (_i64, [_vp, _vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp]),
+    "bshuf_decompress_lz4_batch_dev_dlen": (_i64, [_vp, _vp, _vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz,
+                                                   _vp, _vp]),
     "bshuf_synth_fill_dev": (_i64, [_vp, _sz, _int, _u64, _u64, _vp]),
     "bshuf_prof_enable": (None, [_int]),
     "bshuf_prof_only": (None, [ctypes.c_char_p]),

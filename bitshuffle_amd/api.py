@@ -189,10 +189,14 @@ def compress_lz4_dev(t, block_size=0, out=None, workspace=None, result=None, off
 
 
 def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None, result=None,
-                       offsets=None, stream=None, sync=True, elem_size=None):
+                       offsets=None, stream=None, sync=True, elem_size=None, length=None):
     """Device-resident bshuf_decompress_lz4 of the whole uint8 tensor `buf`
     (its length is the exact stream length).  With `elem_size`, `shape` counts
-    elem_size-byte elements and the output is a uint8 tensor of their bytes."""
+    elem_size-byte elements and the output is a uint8 tensor of their bytes.
+    With `length` (a 1-element int64 DEVICE tensor, e.g. compress_lz4_dev's
+    `result` with sync=False), the stream length is read on the device
+    (bshuf_decompress_lz4_dev_dlen) and `buf` is only its capacity: nothing
+    waits on the host between the two calls."""
     torch = _torch()
     size = 1
     for s in shape:
@@ -208,15 +212,23 @@ def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None
     ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
     wsb = workspace.numel() if workspace is not None else 0
     offp = _dptr(offsets) if offsets is not None else None
-    _check(lib.bshuf_decompress_lz4_dev(_dptr(buf), buf.numel(), _dptr(out), size,
-                                        es, block_size, ws, wsb, _dptr(result),
-                                        offp, _stream(stream)))
+    if length is None:
+        _check(lib.bshuf_decompress_lz4_dev(_dptr(buf), buf.numel(), _dptr(out), size,
+                                            es, block_size, ws, wsb, _dptr(result),
+                                            offp, _stream(stream)))
+    else:
+        if length.dtype != torch.int64 or length.numel() < 1 or length.device != buf.device:
+            raise ValueError("length must be an int64 tensor on the stream's device")
+        _check(lib.bshuf_decompress_lz4_dev_dlen(_dptr(buf), _dptr(length), buf.numel(), _dptr(out),
+                                                 size, es, block_size, ws, wsb, _dptr(result),
+                                                 offp, _stream(stream)))
     if not sync:
         return out, result
     count = int(result.item())
     if count < 0:
         _fail(count)
-    if count != buf.numel():
+    want = buf.numel() if length is None else int(length.reshape(-1)[0].item())
+    if count != want:
         raise BshufError("Decompressed different number of bytes than input buffer size."
                          "Input buffer %d, decompressed %d." % (buf.numel(), count), count)
     return out
@@ -270,12 +282,15 @@ def compress_lz4_batch_dev(tensors, block_size=0, outs=None, workspace=None, off
 
 
 def decompress_lz4_batch_dev(bufs, shapes, dtype, block_size=0, outs=None, workspace=None,
-                             stream=None, sync=True, elem_size=None):
+                             stream=None, sync=True, elem_size=None, lengths=None):
     """bshuf_decompress_lz4_batch_dev: each uint8 device tensor of `bufs` is one
     whole framed stream; returns the decoded tensors (sync=True), or (outs,
     results) with per-stream consumed byte counts / error codes.  With
     `elem_size`, shapes count elem_size-byte elements and the outputs are
-    uint8 tensors of their bytes."""
+    uint8 tensors of their bytes.  With `lengths` (an int64 DEVICE tensor of
+    len(bufs), e.g. compress_lz4_batch_dev's results with sync=False), the
+    stream lengths are read on the device (bshuf_decompress_lz4_batch_dev_dlen)
+    and each buffer is only its stream's capacity."""
     torch = _torch()
     if not bufs:
         return []
@@ -305,11 +320,20 @@ def decompress_lz4_batch_dev(bufs, shapes, dtype, block_size=0, outs=None, works
     pnb, keep4 = _size_array(nbytes)
     ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
     wsb = workspace.numel() if workspace is not None else 0
-    _check(lib.bshuf_decompress_lz4_batch_dev(pin, pnb, pout, psz, len(bufs), es, block_size, ws,
-                                              wsb, _dptr(results), _stream(stream)))
+    if lengths is None:
+        _check(lib.bshuf_decompress_lz4_batch_dev(pin, pnb, pout, psz, len(bufs), es, block_size, ws,
+                                                  wsb, _dptr(results), _stream(stream)))
+    else:
+        if lengths.dtype != torch.int64 or lengths.numel() < len(bufs):
+            raise ValueError("lengths must be an int64 device tensor with one entry per stream")
+        _check(lib.bshuf_decompress_lz4_batch_dev_dlen(pin, _dptr(lengths), pnb, pout, psz, len(bufs),
+                                                       es, block_size, ws, wsb, _dptr(results),
+                                                       _stream(stream)))
     if not sync:
         return outs, results
     counts = results.cpu().tolist()
+    if lengths is not None:
+        nbytes = lengths.reshape(-1)[: len(bufs)].cpu().tolist()
     for c, nb in zip(counts, nbytes):
         if c < 0:
             _fail(c)

@@ -85,8 +85,8 @@ size_t dec_ws(const Plan& p, int64_t blocks_end, int64_t in_nbytes, bool need_in
 // kernels working in such re-mapped workspaces produced wrong results early in
 // a process (round-2 host-path defect, DESIGN.md §4.2: 16 of 40 fresh HDF5
 // regression processes with the default pool, 0 of 40 with a pool that never
-// trims).  BSHUF_DIAG_POOL=default brings the default pool back for that
-// experiment only (tools/h5_repro.sh).  This is a WORKAROUND for re-mapping
+// trims).  In the diagnostic build only, BSHUF_DIAG_POOL=default brings the
+// default pool back for that experiment (tools/h5_repro.sh).  This is a WORKAROUND for re-mapping
 // behaviour whose mechanism is not understood, not a proven
 // root cause.  What the pool keeps is capped at the largest single workspace
 // requested so far (pool_keep): one call's worth stays mapped, not every
@@ -112,7 +112,11 @@ hipMemPool_t workspace_pool() {
     tried = true;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+#ifdef BSHUF_DIAG
     const char* e = getenv("BSHUF_DIAG_POOL");
+#else
+    const char* e = nullptr;
+#endif
     if (e && !strcmp(e, "default")) {
         (void)hipDeviceGetDefaultMemPool(&pool, dev);
         g_pool_is_default = true;
@@ -253,10 +257,12 @@ size_t bshuf_decompress_lz4_dev_workspace(size_t in_nbytes, size_t size, size_t 
     return dec_ws(p, cb > 0 ? cb : 0, (int64_t)in_nbytes, true, nullptr, nullptr);
 }
 
-int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, size_t size,
-                                 size_t elem_size, size_t block_size, void* ws, size_t ws_bytes,
-                                 int64_t* d_result, const uint64_t* block_offsets,
-                                 void* stream) {
+// in_nbytes: the stream's readable bytes -- or, with dlen, the capacity of
+// `in`, the length itself being read by the kernels from *dlen
+static int64_t decompress_dev(const void* in, size_t in_nbytes, const int64_t* dlen, void* out,
+                              size_t size, size_t elem_size, size_t block_size, void* ws,
+                              size_t ws_bytes, int64_t* d_result, const uint64_t* block_offsets,
+                              void* stream) {
     Plan p;
     const int64_t r = make_plan(size, elem_size, block_size, p);
     if (r) return r;
@@ -277,15 +283,33 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
     dec_ws(p, cb, (int64_t)in_nbytes, need_index, &b, (uint8_t*)ws);
     const uint8_t* i8 = (const uint8_t*)in;
     if (need_index) {
-        if (launch_index(i8, cb, p.L, b, s) != hipSuccess) return kErrHip;
+        if (launch_index(i8, cb, p.L, b, s, dlen, (int64_t)in_nbytes, p.tail) != hipSuccess)
+            return kErrHip;
     } else {
         b.offs = const_cast<uint64_t*>(block_offsets);
         b.idx_err = nullptr;
     }
-    if (launch_decode(i8, (int64_t)in_nbytes, (uint8_t*)out, p.L, p.tail, b, d_result, s) !=
+    if (launch_decode(i8, (int64_t)in_nbytes, (uint8_t*)out, p.L, p.tail, b, d_result, s, dlen) !=
         hipSuccess)
         return kErrHip;
     return 0;
+}
+
+int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, size_t size,
+                                 size_t elem_size, size_t block_size, void* ws, size_t ws_bytes,
+                                 int64_t* d_result, const uint64_t* block_offsets,
+                                 void* stream) {
+    return decompress_dev(in, in_nbytes, nullptr, out, size, elem_size, block_size, ws, ws_bytes,
+                          d_result, block_offsets, stream);
+}
+
+int64_t bshuf_decompress_lz4_dev_dlen(const void* in, const int64_t* d_in_nbytes, size_t in_capacity,
+                                      void* out, size_t size, size_t elem_size, size_t block_size,
+                                      void* ws, size_t ws_bytes, int64_t* d_result,
+                                      const uint64_t* block_offsets, void* stream) {
+    if (!d_in_nbytes) return kErrUnsupported;
+    return decompress_dev(in, in_capacity, d_in_nbytes, out, size, elem_size, block_size, ws,
+                          ws_bytes, d_result, block_offsets, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -454,10 +478,12 @@ size_t bshuf_decompress_lz4_batch_dev_workspace(const size_t* in_nbytes, const s
     return dec_batch_ws(bp, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
-int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_nbytes,
-                                       void* const* out, const size_t* sizes, size_t count,
-                                       size_t elem_size, size_t block_size, void* ws,
-                                       size_t ws_bytes, int64_t* d_results, void* stream) {
+// in_nbytes: per stream, its readable bytes -- or, with dlens (device), the
+// capacity of in[i], the length itself being dlens[i]
+static int64_t decompress_batch(const void* const* in, const size_t* in_nbytes, const int64_t* dlens,
+                                void* const* out, const size_t* sizes, size_t count,
+                                size_t elem_size, size_t block_size, void* ws, size_t ws_bytes,
+                                int64_t* d_results, void* stream) {
     BatchPlan bp;
     const int64_t r = make_batch(in, out, sizes, in_nbytes, count, elem_size, block_size, bp);
     if (r) return r;
@@ -467,9 +493,9 @@ int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_n
     if ((int64_t)bp.L.bs * bp.L.E > max_lds_decode_bytes()) {
         // blocks above the LDS decoder's size: one stream at a time
         for (size_t i = 0; i < count; i++) {
-            const int64_t e = bshuf_decompress_lz4_dev(in[i], in_nbytes[i], out[i], sizes[i], elem_size,
-                                                       block_size, nullptr, 0, d_results + i, nullptr,
-                                                       stream);
+            const int64_t e = decompress_dev(in[i], in_nbytes[i], dlens ? dlens + i : nullptr, out[i],
+                                             sizes[i], elem_size, block_size, nullptr, 0, d_results + i,
+                                             nullptr, stream);
             if (e) return e;
         }
         return 0;
@@ -483,12 +509,31 @@ int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_n
     uint32_t *blk_seg = nullptr, *chunk_seg = nullptr;
     dec_batch_ws(bp, &b, &dsegs, &blk_seg, &chunk_seg, (uint8_t*)ws);
     if (stage_upload(bp.segs.data(), count * sizeof(Seg), dsegs, s) != hipSuccess ||
+        (dlens && launch_seg_dlen(dsegs, dlens, (int)count, s) != hipSuccess) ||
         launch_seg_map(dsegs, (int)count, blk_seg, false, s) != hipSuccess ||
         launch_seg_map(dsegs, (int)count, chunk_seg, true, s) != hipSuccess ||
         launch_index_batch(dsegs, (int)count, chunk_seg, bp.L, bp.nchunks, b, s) != hipSuccess ||
-        launch_decode_batch(dsegs, bp.segs.data(), (int)count, blk_seg, bp.L, b, s) != hipSuccess)
+        launch_decode_batch(dsegs, bp.segs.data(), (int)count, blk_seg, bp.L, b, s, dlens) != hipSuccess)
         return kErrHip;
     return 0;
+}
+
+int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_nbytes,
+                                       void* const* out, const size_t* sizes, size_t count,
+                                       size_t elem_size, size_t block_size, void* ws,
+                                       size_t ws_bytes, int64_t* d_results, void* stream) {
+    return decompress_batch(in, in_nbytes, nullptr, out, sizes, count, elem_size, block_size, ws,
+                            ws_bytes, d_results, stream);
+}
+
+int64_t bshuf_decompress_lz4_batch_dev_dlen(const void* const* in, const int64_t* d_in_nbytes,
+                                            const size_t* in_capacity, void* const* out,
+                                            const size_t* sizes, size_t count, size_t elem_size,
+                                            size_t block_size, void* ws, size_t ws_bytes,
+                                            int64_t* d_results, void* stream) {
+    if (!d_in_nbytes) return kErrUnsupported;
+    return decompress_batch(in, in_capacity, d_in_nbytes, out, sizes, count, elem_size, block_size,
+                            ws, ws_bytes, d_results, stream);
 }
 
 int64_t bshuf_synth_fill_dev(void* out, size_t n_elem, int gen, uint64_t first, uint64_t seed,

@@ -19,8 +19,9 @@
 // used, so completion never rests on a copy engine's event.  (They were not the
 // cause of the round-2 stale-result defect -- re-mapped stream-ordered pool
 // memory was, DESIGN.md §4.2 -- but the flag protocol makes every host-visible
-// byte's completion checkable.)  BSHUF_HOST_XFER=dma / dma_staged / dma_fenced
-// bring DMA copies back for that experiment only (tools/h5_repro.sh).
+// byte's completion checkable.)  In the DIAGNOSTIC build only (make diag,
+// -DBSHUF_DIAG), BSHUF_HOST_XFER=dma / dma_staged / dma_fenced bring DMA copies
+// back for that experiment (tools/h5_repro.sh); the product has one transport.
 #include <hip/hip_runtime.h>
 #include <sched.h>
 #include <stdio.h>
@@ -143,13 +144,16 @@ __global__ __launch_bounds__(kXferThreads) void k_xfer(XferArgs a) {
     }
 }
 
+#ifdef BSHUF_DIAG
 // The round-2 mitigation, kept for the DMA experiment only: a system-scope
 // release + acquire per workgroup (256 workgroups, hoping to meet every XCD).
 __global__ __launch_bounds__(64) void k_l2_flush_all() { __threadfence_system(); }
+#endif
 
 // ---------------------------------------------------------------------------
 // per-thread state
 // ---------------------------------------------------------------------------
+#ifdef BSHUF_DIAG
 enum class Xfer { kKernel, kDma, kDmaFenced, kDmaStaged };
 
 Xfer xfer_mode() {
@@ -163,6 +167,7 @@ Xfer xfer_mode() {
     }
     return (Xfer)m;
 }
+#endif  // (the product has the kernel transport only)
 
 std::atomic<uint64_t> g_stat_late{0};    // flags not yet all set when the event said done
 std::atomic<uint64_t> g_stat_pieces{0};  // staged pieces moved
@@ -318,6 +323,7 @@ HostCtx* host_ctx() {
     return &t_ctx;
 }
 
+#ifdef BSHUF_DIAG
 hipError_t dma_fence(HostCtx& c) {
     if (xfer_mode() != Xfer::kDmaFenced) return hipSuccess;
     hipLaunchKernelGGL(k_l2_flush_all, dim3(256), dim3(64), 0, c.s);
@@ -368,16 +374,19 @@ bool d2h_staged(HostCtx& c, uint8_t* dst, const uint8_t* src, size_t n) {
     }
     return true;
 }
+#endif  // BSHUF_DIAG
 
 // Host bytes [lo, hi) of `src` to the device buffer `dst` (same offsets).
 // Returns once the last piece is enqueued; its slot is released later.
 bool h2d(HostCtx& c, uint8_t* dst, const uint8_t* src, uint64_t lo, uint64_t hi) {
     if (hi <= lo) return true;
+#ifdef BSHUF_DIAG
     if (xfer_mode() == Xfer::kDmaStaged) return h2d_staged(c, dst, src, lo, hi);
     if (xfer_mode() != Xfer::kKernel) {
         const bool ok = hipMemcpyAsync(dst + lo, src + lo, hi - lo, hipMemcpyHostToDevice, c.s) == hipSuccess;
         return ok && dma_fence(c) == hipSuccess;
     }
+#endif
     lo &= ~(uint64_t)15;  // re-sending bytes already sent is harmless; keeps both ends aligned
     for (uint64_t off = lo; off < hi; off += kPiece) {
         const size_t len = (size_t)std::min<uint64_t>(kPiece, hi - off);
@@ -393,12 +402,14 @@ bool h2d(HostCtx& c, uint8_t* dst, const uint8_t* src, uint64_t lo, uint64_t hi)
 // n device bytes at `src` (16-aligned) to host `dst`; complete on return.
 bool d2h(HostCtx& c, uint8_t* dst, const uint8_t* src, size_t n) {
     if (n == 0) return true;
+#ifdef BSHUF_DIAG
     if (xfer_mode() == Xfer::kDmaStaged) return d2h_staged(c, dst, src, n);
     if (xfer_mode() != Xfer::kKernel) {
         if (dma_fence(c) != hipSuccess) return false;
         return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c.s) == hipSuccess &&
                hipStreamSynchronize(c.s) == hipSuccess;
     }
+#endif
     if (!c.settle(0) || !c.settle(1)) return false;
     const size_t np = (n + kPiece - 1) / kPiece;
     auto issue = [&](size_t i) {
@@ -417,20 +428,27 @@ bool d2h(HostCtx& c, uint8_t* dst, const uint8_t* src, size_t n) {
 
 // The 8-byte device result word of the stream's last kernel.
 bool read_result(HostCtx& c, const int64_t* dres, int64_t& res) {
+#ifdef BSHUF_DIAG
     if (xfer_mode() != Xfer::kKernel) {
         if (dma_fence(c) != hipSuccess) return false;
         return hipMemcpyAsync(&res, dres, 8, hipMemcpyDeviceToHost, c.s) == hipSuccess &&
                hipStreamSynchronize(c.s) == hipSuccess;
     }
+#endif
     return d2h(c, (uint8_t*)&res, (const uint8_t*)dres, 8);
 }
 
-// Stale-result experiment only (BSHUF_DIAG_WS=alloc): the round-2 host path's
-// per-call stream-ordered workspace (api.hip's DevBuf) instead of the thread's
-// cached one; with BSHUF_DIAG_POOL=default it comes from the default pool.
+// Stale-result experiment only, diagnostic build (BSHUF_DIAG_WS=alloc): the
+// round-2 host path's per-call stream-ordered workspace (api.hip's DevBuf)
+// instead of the thread's cached one; with BSHUF_DIAG_POOL=default it comes
+// from the default pool.
 bool diag_alloc_ws() {
+#ifdef BSHUF_DIAG
     static const bool on = getenv("BSHUF_DIAG_WS") != nullptr;
     return on;
+#else
+    return false;
+#endif
 }
 
 int64_t fail(HostCtx& c) {

@@ -147,11 +147,14 @@ struct DecodeBufs {
 };
 int64_t index_chunk_bytes(const Layout& L);
 size_t decode_scan_tmp_bytes(int64_t nchunks);
+// dlen (optional): the stream length lives in device memory (read by the
+// kernels); blocks_end / in_nbytes are then the CAPACITY's, tail the raw tail.
 hipError_t launch_index(const uint8_t* in, int64_t blocks_end, const Layout& L,
-                        const DecodeBufs& b, hipStream_t s);
+                        const DecodeBufs& b, hipStream_t s, const int64_t* dlen = nullptr,
+                        int64_t cap = 0, int64_t tail = 0);
 hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
-                         hipStream_t s);
+                         hipStream_t s, const int64_t* dlen = nullptr);
 // wave-parallel execution of blocks above max_lds_decode_bytes (lz4_decode.hip)
 hipError_t launch_exec_big(const uint8_t* in, const Layout& L, const DecodeBufs& b, uint8_t* shuf,
                            hipStream_t s);
@@ -162,7 +165,11 @@ hipError_t launch_decode_large(const uint8_t* in, int64_t in_nbytes, uint8_t* ou
 hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_seg, const Layout& L,
                               int64_t nchunks, const DecodeBufs& b, hipStream_t s);
 hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
-                               const Layout& L, const DecodeBufs& b, hipStream_t s);
+                               const Layout& L, const DecodeBufs& b, hipStream_t s,
+                               const int64_t* dlens = nullptr);
+// device-held batch stream lengths: segs[i].in_nbytes (the capacity) becomes
+// the readable bytes of dlens[i]; run before the index rebuild
+hipError_t launch_seg_dlen(Seg* segs, const int64_t* dlens, int nsegs, hipStream_t s);
 
 // ---- the reference's internal transpose steps (internals.hip) -------------
 // out[(j * lda + i) * es + t] = in[(i * ldb + j) * es + t]  (bshuf_trans_elem)

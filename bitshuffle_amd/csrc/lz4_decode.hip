@@ -71,7 +71,26 @@ struct IdxArgs {
     uint32_t maxlen;
     int64_t win_lds;     // k_idx_exits' LDS window bytes
     int64_t wsub;        // candidates per k_idx_exits workgroup (gridDim.y of them per chunk)
+    // single stream with its length in device memory (bshuf_decompress_lz4_dev_dlen):
+    // Cb is then resolved on the device from *dlen, the capacity and the raw tail
+    const int64_t* dlen;
+    int64_t cap;
+    int64_t tail;
 };
+
+// Readable stream bytes of a device-held length word: a negative word (an
+// upstream error, e.g. the compress result) reads nothing; never past cap.
+__device__ __forceinline__ int64_t readable_bytes(int64_t d, int64_t cap) {
+    return d < 0 ? 0 : (d < cap ? d : cap);
+}
+
+// Resolves a device-held stream length once per kernel (single stream).
+__device__ __forceinline__ void resolve_len(IdxArgs& x) {
+    if (x.dlen) {
+        x.Cb = max(readable_bytes(*x.dlen, x.cap) - x.tail, (int64_t)0);
+        x.dlen = nullptr;
+    }
+}
 
 struct ChunkLoc {
     const uint8_t* in;
@@ -114,12 +133,19 @@ __global__ __launch_bounds__(64) void k_idx_exits(IdxArgs x, int64_t* __restrict
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
     int win_off = 0;
     const int lane = threadIdx.x;
+    resolve_len(x);
     const ChunkLoc L = chunk_loc(x, blockIdx.x);
     const uint8_t* in = L.in;
     const int64_t Cb = L.Cb, CH = x.CH, W = x.W;
     const uint32_t maxlen = x.maxlen;
     const int64_t s = L.s;
     const int64_t cs = s * CH;
+    if (s > 0 && cs >= Cb) {
+        // past the stream's end (chunks sized by a capacity, device-held
+        // length): no entry, and nothing ever chases from here
+        if (gridDim.y == 1 && lane == 0) exits[blockIdx.x] = kDead;
+        return;
+    }
     const int64_t ce = min(cs + CH, Cb);
     // candidate window [cs, cs + W), split over gridDim.y workgroups of wsub
     // candidates each (large blocks: a window of the largest record does not
@@ -270,9 +296,14 @@ __global__ __launch_bounds__(64) void k_idx_walk(IdxArgs x, int64_t nchunks_tota
                                                  uint64_t* __restrict__ offs, int mode) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchunks_total) return;
+    resolve_len(x);
     const ChunkLoc L = chunk_loc(x, c);
     const int64_t CH = x.CH, Cb = L.Cb;
     const uint32_t maxlen = x.maxlen;
+    if (L.s > 0 && L.s * CH >= Cb) {  // past the stream's end: no headers
+        if (!mode) cnt[c] = 0;
+        return;
+    }
     const int64_t ce = min((L.s + 1) * CH, Cb);
     int64_t p = chunk_entry(L.in, exits + L.c0, L.s, CH, Cb, maxlen);
     if (p == kDead) {
@@ -612,7 +643,16 @@ struct DecArgs {
                         // -1: through registers into the block's own LDS)
     int32_t ip_end;     // VAR & 512: the in-place record region ends at this LDS offset
     int64_t blk0, blk1; // k_seq_scan / k_lz4_decode: this launch's blocks [blk0, blk1)
+    const int64_t* dlen;  // single stream: length in device memory (in_nbytes = capacity)
 };
+
+// The single stream's readable bytes from its device-held length, once per kernel.
+__device__ __forceinline__ void resolve_len(DecArgs& a) {
+    if (a.dlen) {
+        a.in_nbytes = readable_bytes(*a.dlen, a.in_nbytes);
+        a.dlen = nullptr;
+    }
+}
 
 // Where block k lives: its stream's framed bytes, output, token-position area
 // and failure word, its element count and whether it is its stream's last.
@@ -866,6 +906,7 @@ struct SeqOut {
 __global__ __launch_bounds__(256) void k_seq_scan(DecArgs a, int64_t nb) {
     const int64_t k = a.blk0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= a.blk1) return;
+    resolve_len(a);
     const BlockLoc loc = block_loc(a, k, nb, a.segs ? a.blk_seg[k] : 0u);
     const int n = loc.m * a.L.E;
     int64_t o0 = (int64_t)a.offs[k];
@@ -934,6 +975,7 @@ __global__ __launch_bounds__(64) void k_seq_scan_big(DecArgs a, int64_t nb) {
     __shared__ __attribute__((aligned(16))) uint8_t win[kScanWin];
     const int lane = threadIdx.x;
     const int64_t k = blockIdx.x;
+    resolve_len(a);
     const BlockLoc loc = block_loc(a, k, nb, a.segs ? a.blk_seg[k] : 0u);
     const int n = loc.m * a.L.E;
     int64_t o0 = (int64_t)a.offs[k];
@@ -1021,6 +1063,7 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
     int64_t blk = a.blk0 + blockIdx.x;
     const int64_t end = a.blk1;  // this launch's blocks [blk0, end); nb: the whole stream(s)
     if (blk >= end) return;
+    resolve_len(a);
 
     PayRegsT<kIP ? kPayItersIP : kPayIters> R;
     // in place: every record is prefetched (partly, when long) into R
@@ -1261,12 +1304,23 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
 // Result: bytes consumed, or the error of the LAST failing block (the
 // sequential reference keeps overwriting err, src/bitshuffle_core.c:1905).
 // Also copies the raw tail (whose position is only known from the index).
+// A device-held stream length (dlen) that is negative is an upstream error
+// (the compress result word of a chained call): it becomes the result as is.
 __global__ __launch_bounds__(256) void k_decode_finish(const int64_t* __restrict__ status,
                                                        const uint64_t* __restrict__ offs,
                                                        int64_t nblocks, const long long* bad,
                                                        const int64_t* idx_err, const uint8_t* in,
                                                        int64_t in_nbytes, uint8_t* tail_dst,
-                                                       int64_t tail, int64_t* result) {
+                                                       int64_t tail, int64_t* result,
+                                                       const int64_t* dlen) {
+    if (dlen) {
+        const int64_t d = *dlen;
+        if (d < 0) {
+            if (threadIdx.x == 0) *result = d;
+            return;
+        }
+        in_nbytes = readable_bytes(d, in_nbytes);
+    }
     const long long last_bad = *bad;
     const int64_t end = nblocks ? (int64_t)offs[nblocks - 1] + status[nblocks - 1] : 0;
     const bool idx_bad = idx_err && *idx_err != 0;
@@ -1490,10 +1544,10 @@ hipError_t index_impl(const IdxArgs& x, int64_t nb, int64_t nch, int nsegs, cons
 }  // namespace
 
 hipError_t launch_index(const uint8_t* in, int64_t Cb, const Layout& L, const DecodeBufs& b,
-                        hipStream_t s) {
+                        hipStream_t s, const int64_t* dlen, int64_t cap, int64_t tail) {
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     IdxArgs x{in, Cb, L.nblocks(), b.idx_err, nullptr, nullptr, nullptr, b.chunk,
-              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen), idx_wsub(maxlen)};
+              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen), idx_wsub(maxlen), dlen, cap, tail};
     return index_impl(x, L.nblocks(), b.nchunks, 1, b, s);
 }
 
@@ -1501,7 +1555,7 @@ hipError_t launch_index_batch(const Seg* segs, int nsegs, const uint32_t* chunk_
                               int64_t nchunks, const DecodeBufs& b, hipStream_t s) {
     const uint32_t maxlen = (uint32_t)lz4_bound(L.bs * L.E);
     IdxArgs x{nullptr, 0, L.nfull, nullptr, segs, chunk_seg, b.idx_err, b.chunk,
-              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen), idx_wsub(maxlen)};
+              4 + (int64_t)maxlen, maxlen, idx_win_lds(maxlen), idx_wsub(maxlen), nullptr, 0, 0};
     return index_impl(x, L.nfull, nchunks, nsegs, b, s);
 }
 
@@ -1609,14 +1663,25 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
     return e != hipSuccess ? e : dec(0, nb, s);
 }
 
+// Batch streams with device-held lengths: each Seg's in_nbytes (its capacity,
+// uploaded from the host) becomes the readable bytes of its length word.
+__global__ void k_seg_dlen(Seg* __restrict__ segs, const int64_t* __restrict__ dlens, int nsegs) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < nsegs) segs[i].in_nbytes = readable_bytes(dlens[i], segs[i].in_nbytes);
+}
+
 // Batch result per stream: bytes consumed, or the error of its LAST failing
 // block (one workgroup per stream; same rules as k_decode_finish).
 __global__ __launch_bounds__(64) void k_decode_finish_batch(const int64_t* __restrict__ status,
                                                             const uint64_t* __restrict__ offs,
                                                             const long long* bad,
                                                             const int64_t* idx_err, const Seg* segs,
-                                                            int32_t bs, int32_t E) {
+                                                            int32_t bs, int32_t E, const int64_t* dlens) {
     const Seg& g = segs[blockIdx.x];
+    if (dlens && dlens[blockIdx.x] < 0) {  // upstream error (see k_decode_finish)
+        if (threadIdx.x == 0) *g.result = dlens[blockIdx.x];
+        return;
+    }
     const int64_t nb = g.nfull + (g.last ? 1 : 0);
     const long long last_bad = bad[blockIdx.x];
     const int64_t end = nb ? (int64_t)offs[g.first + nb - 1] + status[g.first + nb - 1] : 0;
@@ -1631,7 +1696,7 @@ __global__ __launch_bounds__(64) void k_decode_finish_batch(const int64_t* __res
 
 hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, const Layout& L,
                          int64_t tail_bytes, const DecodeBufs& b, int64_t* d_result,
-                         hipStream_t s) {
+                         hipStream_t s, const int64_t* dlen) {
     const int64_t nb = L.nblocks();
     hipError_t e = dev_fill(b.bad, 0xFF, sizeof(long long), s);  // -1
     if (e != hipSuccess) return e;
@@ -1639,7 +1704,7 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
         const int64_t nmax = (int64_t)L.bs * L.E;
         DecArgs a{in, in_nbytes, b.offs, out, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
                   (int32_t)((nmax + 15) & ~15), b.seq, nullptr, nullptr,
-                  ((uintptr_t)out & 7) == 0 ? 1 : 0, 0, 0, nb};
+                  ((uintptr_t)out & 7) == 0 ? 1 : 0, 0, 0, nb, dlen};
         if (nmax > max_lds_decode_bytes()) {
             // large blocks: validated by the same scan (a wave per block),
             // executed in global memory
@@ -1654,12 +1719,17 @@ hipError_t launch_decode(const uint8_t* in, int64_t in_nbytes, uint8_t* out, con
     ProfScope prof("k_decode_finish", s);
     hipLaunchKernelGGL(k_decode_finish, dim3(1), dim3(64), 0, s, b.status, b.offs, nb,
                        (const long long*)b.bad, (const int64_t*)b.idx_err, in, in_nbytes,
-                       tail_dst, tail_bytes, d_result);
+                       tail_dst, tail_bytes, d_result, dlen);
+    return hipGetLastError();
+}
+
+hipError_t launch_seg_dlen(Seg* segs, const int64_t* dlens, int nsegs, hipStream_t s) {
+    hipLaunchKernelGGL(k_seg_dlen, dim3((unsigned)((nsegs + 255) / 256)), dim3(256), 0, s, segs, dlens, nsegs);
     return hipGetLastError();
 }
 
 hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, const uint32_t* blk_seg,
-                               const Layout& L, const DecodeBufs& b, hipStream_t s) {
+                               const Layout& L, const DecodeBufs& b, hipStream_t s, const int64_t* dlens) {
     const int64_t nb = L.nfull;
     hipError_t e = dev_fill(b.bad, 0xFF, sizeof(long long) * (size_t)nsegs, s);
     if (e != hipSuccess) return e;
@@ -1671,13 +1741,13 @@ hipError_t launch_decode_batch(const Seg* segs, const Seg* hsegs, int nsegs, con
             al8 = al8 && ((uintptr_t)hsegs[i].out & 7) == 0;
         }
         DecArgs a{nullptr, 0, b.offs, nullptr, b.status, b.bad, L, (uint32_t)lz4_bound((int)nmax),
-                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg, al8 ? 1 : 0, 0, 0, nb};
+                  (int32_t)((nmax + 15) & ~15), b.seq, segs, blk_seg, al8 ? 1 : 0, 0, 0, nb, nullptr};
         e = decode_impl(a, nb, aligned, s);
         if (e != hipSuccess) return e;
     }
     ProfScope prof("k_decode_finish", s);
     hipLaunchKernelGGL(k_decode_finish_batch, dim3((unsigned)nsegs), dim3(64), 0, s, b.status, b.offs,
-                       (const long long*)b.bad, (const int64_t*)b.idx_err, segs, L.bs, L.E);
+                       (const long long*)b.bad, (const int64_t*)b.idx_err, segs, L.bs, L.E, dlens);
     return hipGetLastError();
 }
 

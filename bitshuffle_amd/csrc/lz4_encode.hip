@@ -1912,11 +1912,13 @@ hipError_t encode_pipelined(int64_t nb, hipStream_t s, PipeCtx* pc, const Encode
         if (e != hipSuccess) break;
         {
             size_t tmp = b.scan_tmp_bytes;
-            ProfScope prof("scan_block_offsets", pc->side);
+            // "_side": beside the parse (bench.py keeps these apart from the
+            // step's serial kernels)
+            ProfScope prof("scan_block_offsets_side", pc->side);
             e = hipcub::DeviceScan::ExclusiveSum(b.scan_tmp, tmp, b.foot, b.offs, (int)(f1 + 1), pc->side);
         }
         if (e != hipSuccess) break;
-        ProfScope prof("k_compact", pc->side);
+        ProfScope prof("k_compact_side", pc->side);
         hipLaunchKernelGGL(k_compact, dim3((unsigned)((f1 - f0 + kCompactPerWg - 1) / kCompactPerWg)),
                            dim3(256), 0, pc->side, b.scratch, b.slot, b.offs, out, segs, blk_seg,
                            block_offsets, f0, f1);

@@ -32,9 +32,11 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size,
 
 /* ---- device-resident extensions (additive, not in the reference) ----
  *
- * Workspace: pass ws=NULL to let the library allocate (stream-ordered) per
- * call, or pre-allocate bshuf_*_dev_workspace() bytes of device memory (must
- * be 256-byte aligned) so the call performs no allocation and can be captured
+ * Workspace: pass ws=NULL to let the library take it from its own device
+ * memory pool (stream-ordered allocate/free per call; the pool keeps up to the
+ * largest workspace requested so far mapped), or
+ * pre-allocate bshuf_*_dev_workspace() bytes of device memory (must be
+ * 256-byte aligned) so the call performs no allocation and can be captured
  * into a hipGraph.
  *
  * Results are written to *d_result (a DEVICE int64): bytes written (compress),
@@ -48,6 +50,16 @@ int64_t bshuf_decompress_lz4(const void* in, void* out, const size_t size,
  * in_nbytes bounds every read).  `block_offsets` (optional, may be NULL) lets
  * a caller that kept the encoder's index skip that rebuild: bshuf_compress_lz4_dev
  * fills it when non-NULL (nblocks u64 entries = byte offset of each block header).
+ *
+ * bshuf_decompress_lz4_dev_dlen takes the stream length as a DEVICE int64
+ * (d_in_nbytes, read by the kernels when they run -- e.g. the d_result word of
+ * a bshuf_compress_lz4_dev enqueued before it on the same stream), so a
+ * compress -> decompress chain never waits on the host.  Like the reference's
+ * bshuf_decompress_lz4 (src/bitshuffle.c:243-247, which is not told the length
+ * at all), the host passes no length; in_capacity bounds every read (readable
+ * bytes = min(*d_in_nbytes, in_capacity)) and sizes the workspace
+ * (bshuf_decompress_lz4_dev_workspace(in_capacity, ...)).  A negative
+ * *d_in_nbytes (an upstream error) is written to *d_result unchanged.
  */
 size_t bshuf_compress_lz4_dev_workspace(size_t size, size_t elem_size, size_t block_size);
 size_t bshuf_decompress_lz4_dev_workspace(size_t in_nbytes, size_t size, size_t elem_size,
@@ -62,6 +74,10 @@ int64_t bshuf_decompress_lz4_dev(const void* in, size_t in_nbytes, void* out, si
                                  size_t elem_size, size_t block_size, void* ws,
                                  size_t ws_bytes, int64_t* d_result,
                                  const uint64_t* block_offsets, void* stream);
+int64_t bshuf_decompress_lz4_dev_dlen(const void* in, const int64_t* d_in_nbytes, size_t in_capacity,
+                                      void* out, size_t size, size_t elem_size, size_t block_size,
+                                      void* ws, size_t ws_bytes, int64_t* d_result,
+                                      const uint64_t* block_offsets, void* stream);
 
 /* ---- batched device entry points (additive) ----
  *
@@ -89,6 +105,16 @@ int64_t bshuf_decompress_lz4_batch_dev(const void* const* in, const size_t* in_n
                                        void* const* out, const size_t* sizes, size_t count,
                                        size_t elem_size, size_t block_size, void* ws,
                                        size_t ws_bytes, int64_t* d_results, void* stream);
+/* The same with the stream lengths as a DEVICE array d_in_nbytes[count] (e.g.
+ * the d_results of a bshuf_compress_lz4_batch_dev before it on the stream);
+ * in_capacity[] (host) bounds each stream's reads and sizes the workspace
+ * (bshuf_decompress_lz4_batch_dev_workspace(in_capacity, ...)).  A negative
+ * length is written to that stream's result unchanged. */
+int64_t bshuf_decompress_lz4_batch_dev_dlen(const void* const* in, const int64_t* d_in_nbytes,
+                                            const size_t* in_capacity, void* const* out,
+                                            const size_t* sizes, size_t count, size_t elem_size,
+                                            size_t block_size, void* ws, size_t ws_bytes,
+                                            int64_t* d_results, void* stream);
 
 /* Synthetic benchmark inputs of SURVEY.md 8(d), generated on the device
  * (counter based, identical to the CPU definition): gen 0 = int32 ramp,

@@ -7,7 +7,10 @@ tests/golden/vectors/:
     byte patterns) -> the reference's bitshuffle output and bitshuffle+LZ4
     stream, stored whole for small cases and as SHA-256 digests for the
     BASELINE.json full-size configs (64 MiB int32 ramp, 4 GiB int16 G1,
-    16 GiB float32 G2, 32 MiB G1 chunks of config 4).
+    16 GiB float32 G2, 32 MiB G1 chunks of config 4), and for the element-size /
+    block-size modes (MODES: G1 int16 bytes re-read as E = 3 / 12 elements, or
+    framed with 256 KiB blocks -- bench.py's --elem-size / --block-size lines
+    at 4 GiB, and the 1 GiB workload of tools/ab.py with AB_ELEM).
 Inputs are regenerated from their counter-based definition at test time, so
 only outputs are stored.  Run:  python tests/golden/make_vectors.py [--full]
 """
@@ -81,16 +84,46 @@ FULL = [
      for c in (0, 1, 2, 3, 511, 1023)]
 
 
+# G1 int16 (seed 12345) generated for n_i16 elements, its first `nbytes` bytes
+# framed as `elem_size`-byte elements with block size `bs` (0 = default)
+def _mode(name, n_i16, nbytes, E, bs):
+    return dict(name=name, gen="g1", n=n_i16, nbytes=nbytes, elem_size=E, bs=bs)
+
+
+MODES = [
+    # tools/ab.py 1 GiB with AB_ELEM=E: x = int16[2**29] -> bytes[:(2**30 // E) * E]
+    _mode("mode_ab_g1_1GiB_E3", 1 << 29, (1 << 30) // 3 * 3, 3, 0),
+    _mode("mode_ab_g1_1GiB_E12", 1 << 29, (1 << 30) // 12 * 12, 12, 0),
+    _mode("mode_g1_1GiB_E2_bs131072", 1 << 29, 1 << 30, 2, 131072),
+    # bench.py --elem-size E / --block-size B at 4 GiB: n = 2**32 // E // 8 * 8
+    _mode("mode_bench_g1_4GiB_E3", 1 << 31, (1 << 32) // 3 // 8 * 8 * 3, 3, 0),
+    _mode("mode_bench_g1_4GiB_E12", 1 << 31, (1 << 32) // 12 // 8 * 8 * 12, 12, 0),
+    _mode("mode_bench_g1_4GiB_E2_bs131072", 1 << 31, 1 << 32, 2, 131072),
+]
+
+
+def mode_input(o, spec):
+    """The mode's input bytes viewed as its elements (must match
+    tests/vectors.py:mode_input)."""
+    raw = o.gen_g1(spec["n"], 0, spec.get("seed", 12345)).view(np.uint8)[: spec["nbytes"]]
+    E = spec["elem_size"]
+    return raw.view(np.dtype("V%d" % E)) if E != 2 else raw.view(np.int16)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="also compute full-size digests")
+    ap.add_argument("--modes", action="store_true", help="also compute element/block-size mode digests")
     args = ap.parse_args()
     o, r = Oracle(), Reference()
     os.makedirs(VEC, exist_ok=True)
-    out = {"small": [], "full": []}
+    out = {"small": [], "full": [], "modes": []}
     path = os.path.join(HERE, "vectors.json")
     if os.path.exists(path):
-        out["full"] = json.load(open(path)).get("full", [])
+        old = json.load(open(path))
+        for k, v in old.items():
+            if k != "small":
+                out[k] = v
     for spec in SMALL:
         a = make_input(o, spec)
         shuf = r.bitshuffle(a, spec["bs"])
@@ -120,6 +153,20 @@ def main():
             del a
             out["full"].append(e)
             print(e["name"], e.get("compressed_len"), flush=True)
+    if args.modes:
+        out["modes"] = []
+        for spec in MODES:
+            a = mode_input(o, spec)
+            comp = r.compress_lz4(a, spec["bs"])
+            e = dict(spec)
+            e.update(size=int(a.size), input_sha256=sha(a), compressed_len=int(comp.size),
+                     compressed_sha256=sha(comp))
+            # the 1 GiB cases: our oracle restatement must agree too
+            if spec["nbytes"] <= (1 << 30):
+                assert o.compress_lz4(a, spec["bs"]).tobytes() == comp.tobytes(), spec["name"]
+            del comp, a
+            out["modes"].append(e)
+            print(e["name"], e["compressed_len"], flush=True)
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
 

@@ -556,6 +556,74 @@ def test_pipelined_encode_matches_oracle(bs, oracle, torch):
 
 
 # ------------------------------------------------------------------ batch API
+def test_device_length_entry_points(bs, oracle, torch):
+    """bshuf_decompress_lz4_dev_dlen / _batch_dev_dlen: the stream length is a
+    DEVICE int64 (the compress result word), the buffer only its capacity.
+    Oracle streams (partial block + raw tail, E = 2 and 3, several block
+    sizes) decode exactly with the same result as the host-length entry
+    point; a negative length (upstream error) comes back unchanged; a length
+    past the capacity is clamped to it; corrupt bytes give the host-length
+    decoder's code."""
+    for E, n, block in [(2, 9 * 4096 + 13, 0), (2, 300000 + 5, 0), (3, 40000 + 3, 0),
+                        (2, 5 * 2048 + 7, 2048), (1, 100, 0), (2, 0, 0)]:
+        raw = oracle.gen_g1((n * E + 1) // 2, 0, 12345).view(np.uint8)[: n * E]
+        a = view_e(raw, E)
+        want = oracle.compress_lz4(a, block)
+        cap = bs.compress_lz4_bound(n, E, block)
+        buf = torch.zeros(max(cap, 1), dtype=torch.uint8, device="cuda")
+        x = torch.from_numpy(raw.copy()).cuda()
+        _, res = bs.compress_lz4_dev(x, block_size=block, out=buf, sync=False, elem_size=E)
+        y, r = bs.decompress_lz4_dev(buf, (n,), torch.uint8, block_size=block, sync=False,
+                                     elem_size=E, length=res)
+        assert int(res.item()) == want.size and int(r.item()) == want.size, (E, n, block)
+        assert buf[: want.size].cpu().numpy().tobytes() == want.tobytes()
+        assert y.cpu().numpy().tobytes() == raw.tobytes(), (E, n, block)
+        # same through the convenience path (sync: checks consumed == length)
+        y2 = bs.decompress_lz4_dev(buf, (n,), torch.uint8, block_size=block, elem_size=E, length=res)
+        assert torch.equal(y2, y)
+    # negative length word: returned as the result, nothing decoded
+    a = oracle.gen_g1(3 * 4096 + 11)
+    enc = oracle.compress_lz4(a)
+    buf = torch.from_numpy(enc.copy()).cuda()
+    neg = torch.tensor([-81], dtype=torch.int64, device="cuda")
+    _, r = bs.decompress_lz4_dev(buf, a.shape, torch.int16, sync=False, length=neg)
+    assert int(r.item()) == -81
+    # length past the capacity: clamped to the buffer (= the exact stream here)
+    big = torch.tensor([enc.size + 12345], dtype=torch.int64, device="cuda")
+    y, r = bs.decompress_lz4_dev(buf, a.shape, torch.int16, sync=False, length=big)
+    assert int(r.item()) == enc.size and y.cpu().numpy().tobytes() == a.tobytes()
+    # a corrupt stream: the host-length decoder's code
+    bad = enc.copy()
+    bad[4 + 40] ^= 0x5A  # inside block 0's payload
+    bad[-30:] = 0        # and the tail end
+    bbuf = torch.from_numpy(bad).cuda()
+    with pytest.raises(RuntimeError) as single:
+        bs.decompress_lz4_dev(bbuf, a.shape, torch.int16)
+    ln = torch.tensor([bad.size], dtype=torch.int64, device="cuda")
+    _, r = bs.decompress_lz4_dev(bbuf, a.shape, torch.int16, sync=False, length=ln)
+    assert int(r.item()) == single.value.args[1]
+    # batch: capacities from the bound, lengths from the compress results
+    sizes = [3 * 4096 + 1005, 0, 17, 4096, 9 * 4096 + 13, 123457]
+    arrs = [oracle.gen_g1(m, 1000 * i, 12345 + i) for i, m in enumerate(sizes)]
+    for block in (0, 2048):
+        xs = [torch.from_numpy(v.copy()).cuda() for v in arrs]
+        outs, res = bs.compress_lz4_batch_dev(xs, block, sync=False)
+        dec, dres = bs.decompress_lz4_batch_dev(outs, [v.shape for v in arrs], torch.int16, block,
+                                                sync=False, lengths=res)
+        want = [oracle.compress_lz4(v, block).size for v in arrs]
+        assert res.cpu().tolist() == want and dres.cpu().tolist() == want, block
+        for v, d in zip(arrs, dec):
+            assert d.cpu().numpy().tobytes() == v.tobytes(), (v.size, block)
+        # one upstream error in the batch: only that stream reports it
+        res2 = res.clone()
+        res2[2] = -91
+        _, dres = bs.decompress_lz4_batch_dev(outs, [v.shape for v in arrs], torch.int16, block,
+                                              sync=False, lengths=res2)
+        got = dres.cpu().tolist()
+        assert got[2] == -91 and [g for i, g in enumerate(got) if i != 2] == \
+            [w for i, w in enumerate(want) if i != 2]
+
+
 def test_batch_api_matches_oracle(bs, oracle, torch):
     """bshuf_*_lz4_batch_dev: streams of different lengths (partial blocks,
     raw tails, an empty one, one smaller than a block) in ONE launch each way;

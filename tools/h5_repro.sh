@@ -10,7 +10,14 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 gcc -O2 -I/opt/conda/include tests/h5_harness.c -L/opt/conda/lib -lhdf5 -Wl,-rpath,/opt/conda/lib \
     -o /tmp/h5h || exit 1
-export HDF5_PLUGIN_PATH=${PLUGIN_DIR:-$PWD/bitshuffle_amd} H5H_DUMP=1 H5H_PASSES=$P
+# the transport / pool switches exist in the DIAGNOSTIC library only (make -C
+# bitshuffle_amd diag): the plugin (rpath $ORIGIN) is run beside a copy of it
+if [ -z "$PLUGIN_DIR" ]; then
+  PLUGIN_DIR=/tmp/h5diag_plugin; mkdir -p $PLUGIN_DIR
+  cp bitshuffle_amd/libh5bshuf_mi355x.so $PLUGIN_DIR/ &&
+  cp bitshuffle_amd/libbitshuffle_mi355x_diag.so $PLUGIN_DIR/libbitshuffle_mi355x.so || exit 1
+fi
+export HDF5_PLUGIN_PATH=$PLUGIN_DIR H5H_DUMP=1 H5H_PASSES=$P
 out=gpurun_out/h5_repro.log
 for mode in $MODES; do
   # mode = transport[+allocws][+defaultpool]: the round-2 per-call

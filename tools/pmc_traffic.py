@@ -9,7 +9,10 @@ read 1/1.63 (x1.63).  WRITE_SIZE (KB) is taken as is (exact for coalesced and
 positions, count ~3.4x their bytes).
 Writes profiles/pmc_traffic.json: {kernel: bytes per launch}, which bench.py
 reports as roofline.traffic for the dominant kernel.
-Usage: python tools/pmc_traffic.py gpurun_out/<tag> [out.json]"""
+Usage: python tools/pmc_traffic.py gpurun_out/<tag> [out.json] [GiB gen elem_size block_size]
+The workload (default: 4 GiB G1, element size 2, default blocks -- config 2)
+is recorded as "_workload"; bench.py attaches the traffic only to a line of
+that same workload."""
 import collections
 import csv
 import glob
@@ -35,6 +38,11 @@ res = {"_method": "per launch: c*FETCH_SIZE*1024 + WRITE_SIZE*1024 bytes, c = 2 
                   "profiles/r03/fetch_probe/calibration.json); from rocprofv3 --pmc passes over "
                   "tools/run_codec_once.py",
        "_source": d}
+wl = sys.argv[3:7] if len(sys.argv) > 6 else ["4", "1", "2", "0"]
+res["_workload"] = {"gen": int(wl[1]), "bytes_per_call": int(float(wl[0]) * (1 << 30)),
+                    "elem_size": int(wl[2]), "block_size": int(wl[3]),
+                    "what": "tools/run_codec_once.py %s both %s (elem_size %s, block_size %s)" % (
+                        wl[0], wl[1], wl[2], wl[3])}
 for k, c in vals.items():
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         f = sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])

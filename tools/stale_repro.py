@@ -12,6 +12,9 @@ fine-grained memory), dma (hipMemcpyAsync to/from the per-thread device
 buffers, no cache maintenance), dma_fenced (dma + the round-2 256-workgroup
 system-scope release/acquire kernel around every copy).
 
+The switches exist in the DIAGNOSTIC library only: run with
+BSHUF_LIB=bitshuffle_amd/libbitshuffle_mi355x_diag.so (make -C bitshuffle_amd diag).
+
 usage: python tools/stale_repro.py [--procs N] [--passes P] mode [mode ...]
 """
 import json
