@@ -584,13 +584,13 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
             // wave -- so no sequence's writes come before an earlier
             // sequence's reads; the scan's margin test keeps every write below
             // every later sequence's record bytes
-            const uint64_t sm = ballot(lit > 0 && lit <= 16);
             uint64_t lm = ballot(lit > 16), done = 0;
+            const uint64_t sm = ballot(lit > 0) & ~lm;
             for (;;) {
                 const int l = lm ? ffs64(lm) : kWave;
                 const uint64_t below = l >= kWave ? ~0ull : ((1ull << l) - 1ull);
                 if (sm & below & ~done) {
-                    if (((sm & below & ~done) >> lane) & 1ull) Cb.copy16(lsrc, D, op, lit);
+                    if (__builtin_amdgcn_inverse_ballot_w64(sm & below & ~done)) Cb.copy16(lsrc, D, op, lit);
                 }
                 if (l >= kWave) break;
                 done = below | (1ull << l);
@@ -600,28 +600,32 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
             }
         }
         // ---- matches, in batches of mutually independent sequences
+        // A later sequence joins the batch when the bytes its match reads
+        // from before its own output ([mop - off, rend), rend = mop - off +
+        // min(ml, off): a self-overlapping match makes the rest itself) were
+        // all final before the batch started; self-overlapping and long
+        // matches run one after another by the wave (coop), short ones per
+        // lane.  Every per-lane test is made once per 64 sequences; a batch
+        // costs one readlane and one compare, the rest is scalar mask work
+        // (inverse ballots turn the masks back into lane predicates).
         const int mop = op + lit;
-        uint64_t todo = (ABL & 2) ? 0ull : ballot(ml > 0);
+        const int rend = mop - off + min(ml, off);
+        const uint64_t mm = (ABL & 2) ? 0ull : ballot(ml > 0);
+        const uint64_t cmask = mm & (ballot(ml > 16) | ballot(off < ml));  // only the head can overlap itself
+        uint64_t todo = mm;
         while (todo) {
             const int f = ffs64(todo);
             const int opf = __builtin_amdgcn_readlane(mop, f);
-            // a later sequence joins the batch when the bytes its match reads
-            // from before its own output ([mop - off, mop - off + min(ml, off)):
-            // a self-overlapping match makes the rest itself) were all final
-            // before the batch started; self-overlapping and long matches run
-            // one after another by the wave (coop), short ones per lane
-            const bool stop = lane > f && ml > 0 && mop - off + min(ml, off) > opf;
-            const uint64_t sm = ballot(stop);
-            const int g = sm ? ffs64(sm) : kWave;
-            const bool inb = lane >= f && lane < g && ml > 0;
-            const bool coop = inb && (ml > 16 || off < ml);  // only the head can overlap itself
-            if (inb && !coop) lane_copy16(D, mop - off, D, mop, ml);
-            for (uint64_t cm = ballot(coop); cm; cm &= cm - 1) {
+            const uint64_t above = ~((2ull << f) - 1ull);  // lanes > f (none for f = 63)
+            const uint64_t sm = ballot(rend > opf) & mm & above;
+            const uint64_t batch = todo & (sm ? (1ull << ffs64(sm)) - 1ull : ~0ull);
+            if (__builtin_amdgcn_inverse_ballot_w64(batch & ~cmask)) lane_copy16(D, mop - off, D, mop, ml);
+            for (uint64_t cm = batch & cmask; cm; cm &= cm - 1) {
                 const int l = ffs64(cm);
                 wave_match(D, __builtin_amdgcn_readlane(mop, l), __builtin_amdgcn_readlane(off, l),
                            __builtin_amdgcn_readlane(ml, l), lane);
             }
-            todo &= g >= kWave ? 0ull : (~0ull << g);
+            todo &= ~batch;
         }
     }
 }

@@ -804,6 +804,85 @@ __device__ __forceinline__ int retest_chain(int& ip, int& ref, int& mc, int& lit
     return code;
 }
 
+// The hand-off from a search match to the re-test chain (OPT & 131072): the
+// catch-up's first 64 bytes back (lz4/lz4.c:1105-1109) and the first count
+// window (lz4/lz4.c:1111-1118 with LZ4_count, :680-703) in ONE LDS round trip
+// and one straight line -- the compiled catch_and_count spends ~100
+// instructions and several exec-mask regions on the same work.  Counting
+// starts at mpos itself: its 4 bytes are equal (the search just compared
+// them), so lane 0 of the window never differs and the match length beyond
+// kMinMatch is c0 - 4 whatever the catch-up finds.  Outputs:
+//   back  bytes the match extends backwards, 0..63; -1: all 64 tested bytes
+//         are equal (the caller continues the catch-up);
+//   c0    equal bytes from mpos in the first 256-byte window, capped at
+//         mlimit - mpos; 256: all equal and the limit lies beyond (count on);
+//   tail  the a-side dword of every lane of that window (window base mpos).
+// Wait states: v_readlane reads v_xor's result three instructions later; its
+// lane select comes from s_ff1 (SALU); SALU reads of VOP3-compare SGPRs are
+// interlocked.
+__device__ __forceinline__ void search_entry(const int mpos, const int mref, const int anchor,
+                                             const int mlimit, const uint32_t dbase,
+                                             const uint32_t lane4d, const uint32_t lanev, int& back,
+                                             int& c0, uint32_t& tail) {
+    int t0, t1, t2, t3, t4;
+    uint32_t val, vah, vbl, vbh, vba, vbb, vca, vcb, vx;
+    uint64_t ne, bm, sy, sz;
+    asm volatile(
+        "s_and_b32 %[t0], %[mpos], -4\n\t"
+        "s_and_b32 %[t1], %[mref], -4\n\t"
+        "v_add_u32 %[vx], %[t0], %[lane4d]\n\t"
+        "v_add_u32 %[vbh], %[t1], %[lane4d]\n\t"
+        "s_add_u32 %[t2], %[mpos], -1\n\t"
+        "s_add_u32 %[t3], %[mref], -1\n\t"
+        "ds_read_b32 %[val], %[vx]\n\t"
+        "ds_read_b32 %[vah], %[vx] offset:4\n\t"
+        "ds_read_b32 %[vbl], %[vbh]\n\t"
+        "ds_read_b32 %[vbh], %[vbh] offset:4\n\t"
+        /* backward bytes: lane k tests mpos-1-k against mref-1-k */
+        "v_sub_u32 %[vba], %[t2], %[lanev]\n\t"
+        "v_sub_u32 %[vbb], %[t3], %[lanev]\n\t"
+        "v_max_i32 %[vca], 0, %[vba]\n\t"
+        "v_max_i32 %[vcb], 0, %[vbb]\n\t"
+        "v_add_u32 %[vca], %[dbase], %[vca]\n\t"
+        "v_add_u32 %[vcb], %[dbase], %[vcb]\n\t"
+        "ds_read_u8 %[vca], %[vca]\n\t"
+        "ds_read_u8 %[vcb], %[vcb]\n\t"
+        "s_and_b32 %[t0], %[mpos], 3\n\t"
+        "s_and_b32 %[t1], %[mref], 3\n\t"
+        "s_sub_u32 %[t2], %[mlimit], %[mpos]\n\t"
+        "s_max_i32 %[t2], %[t2], 0\n\t"
+        "s_waitcnt lgkmcnt(2)\n\t"
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t0]\n\t"
+        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t1]\n\t"
+        "v_xor_b32 %[vx], %[tail], %[vbl]\n\t"
+        "v_cmp_ne_u32 %[ne], %[tail], %[vbl]\n\t"
+        "v_cmp_le_i32 %[sy], %[anchor], %[vba]\n\t"
+        "v_cmp_le_i32 %[sz], 0, %[vbb]\n\t"
+        "s_ff1_i32_b64 %[t3], %[ne]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readlane_b32 %[t4], %[vx], %[t3]\n\t"
+        "v_cmp_eq_u32 %[bm], %[vca], %[vcb]\n\t"
+        "s_lshl_b32 %[t3], %[t3], 2\n\t"
+        "s_ff1_i32_b32 %[t4], %[t4]\n\t"
+        "s_lshr_b32 %[t4], %[t4], 3\n\t"
+        "s_add_u32 %[t3], %[t3], %[t4]\n\t"
+        "s_cmp_eq_u64 %[ne], 0\n\t"
+        "s_cselect_b32 %[t3], 256, %[t3]\n\t"
+        "s_min_i32 %[c0], %[t3], %[t2]\n\t"
+        "s_and_b64 %[bm], %[bm], %[sy]\n\t"
+        "s_and_b64 %[bm], %[bm], %[sz]\n\t"
+        "s_not_b64 %[bm], %[bm]\n\t"
+        "s_ff1_i32_b64 %[back], %[bm]"
+        : [back] "=&s"(back), [c0] "=&s"(c0), [tail] "=&v"(tail), [t0] "=&s"(t0), [t1] "=&s"(t1),
+          [t2] "=&s"(t2), [t3] "=&s"(t3), [t4] "=&s"(t4), [val] "=&v"(val), [vah] "=&v"(vah),
+          [vbl] "=&v"(vbl), [vbh] "=&v"(vbh), [vba] "=&v"(vba), [vbb] "=&v"(vbb), [vca] "=&v"(vca),
+          [vcb] "=&v"(vcb), [vx] "=&v"(vx), [ne] "=&s"(ne), [bm] "=&s"(bm), [sy] "=&s"(sy),
+          [sz] "=&s"(sz)
+        : [mpos] "s"(mpos), [mref] "s"(mref), [anchor] "s"(anchor), [mlimit] "s"(mlimit),
+          [dbase] "s"(dbase), [lane4d] "v"(lane4d), [lanev] "v"(lanev)
+        : "scc", "memory");
+}
+
 // Greedy LZ4 parse of D[0..n) with table T (zeroed).  Every sequence goes to
 // em.seq() once its match is final, the trailing literal run to em.last().
 // Returns the compressed size, or -1 when the emitter ran out of descriptor
@@ -820,6 +899,8 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
     // the hand-scheduled full search windows (OPT & 16384): LDS block too
     constexpr bool kAsmSearch = !WIDE && !READBACK && (OPT & 16384) != 0 && (OPT & 512) == 0 &&
                                 !std::is_same<Blk, GblBlk>::value;
+    // the search-match -> re-test hand-off in one asm block (OPT & 131072)
+    constexpr bool kAsmEntry = kAsmRetest && (OPT & 131072) != 0;
     int op = 0, anchor = 0;
     if (n >= kLz4MinLength) {
         const int limit = n - kMfLimit + 1;  // mflimitPlusOne
@@ -1024,7 +1105,39 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
             STAMP(0);  // (the search's match exits jump here)
             COUNT(0, 1);
             // ------------------------------------------------ catch up + count
-            CountOut co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
+            CountOut co;
+            if constexpr (kAsmEntry) {
+                // one round trip (search_entry); the long cases continue here
+                int back, c0;
+                search_entry(mpos, mref, anchor, mlimit, (uint32_t)(uintptr_t)D,
+                             (uint32_t)(uintptr_t)D + 4u * (uint32_t)lane, (uint32_t)lane, back, c0,
+                             co.tail);
+                if (back < 0) {
+                    // all 64 bytes back are equal: on 64 at a time
+                    for (int base = kWave;; base += kWave) {
+                        const int xa = mpos - 1 - base - lane, xb = mref - 1 - base - lane;
+                        const uint64_t cm = ballot(xa >= anchor && xb >= 0 &&
+                                                   (uint32_t)D[max(xa, 0)] == (uint32_t)D[max(xb, 0)]);
+                        const int run = (~cm) ? ffs64(~cm) : kWave;
+                        back = base + run;
+                        if (run < kWave) break;
+                    }
+                }
+                int total = 0;
+                while (c0 == kWinBytes) {
+                    // the first 256 bytes from mpos are equal: count on
+                    total += kWinBytes;
+                    const uint32_t va = rdw(D, mpos + total + 4 * lane, n);
+                    const uint32_t vb = rdw(D, mref + total + 4 * lane, n);
+                    c0 = window_equal(va, vb, mlimit - (mpos + total));
+                    co.tail = va;
+                }
+                co.back = back;
+                co.cnt = total + c0 - kMinMatch;  // beyond the 4 bytes at mpos
+                co.tail_base = mpos + total;
+            } else {
+                co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
+            }
             ip = mpos - co.back;
             int ref = mref - co.back;
             int mc = co.back + co.cnt;
@@ -1535,7 +1648,7 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                 // descriptors are buffered in VGPRs
                 using Em = typename std::conditional<(VAR & 8192) != 0, EmitDescV, EmitDesc>::type;
                 Em em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768))>(D, n, T, em, lane);
+                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768 | 131072))>(D, n, T, em, lane);
                 KSTAMP(1);
                 if (em.ns > kDescMax) c = -1;  // more sequences than descriptor slots
                 if (c >= 0) {
@@ -1846,10 +1959,19 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         // them: E = 3 / 12 +0.2 % / +0.8 % with them, profiles/r04/asm_search),
         // and their bit-sliced forward transpose (0.694 -> 0.676 / 0.912 ->
         // 0.905 ms, profiles/r04/etr_sliced)
-        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 40960 : 319488)>(a, nb, lds, s);
+        // ... and the search-match -> re-test hand-off in asm (search_entry,
+        // | 131072): k_lz4_encode 2 GiB G1 0.677 -> 0.631 ms, 1 GiB G2 0.911
+        // -> 0.846, 1 GiB as E = 3 1.347 -> 1.218, E = 12 1.229 -> 1.133 per
+        // launch (profiles/r05/r5b); 319488 / 40960 stay as A/B variants
+        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 172032 : 450560)>(a, nb, lds, s);
         if (v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
         if (v == 57344) return launch_enc_t<EK, WIDE, VAR | 57344>(a, nb, lds, s);
+        // + the search-match -> re-test hand-off in asm (search_entry)
+        if (v == 172032) return launch_enc_t<EK, WIDE, VAR | 172032>(a, nb, lds, s);
+        if (v == 450560 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 450560>(a, nb, lds, s);
+        if (v == 450560) return launch_enc_t<EK, WIDE, VAR | 172032>(a, nb, lds, s);
         if (v == 319488 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 319488>(a, nb, lds, s);
+        if (v == 319488) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
     }
     if constexpr ((VAR & 128) == 0) {
         if (!lds_atomics_lane_ordered()) return launch_enc_t<EK, WIDE, VAR | 128>(a, nb, lds, s);

@@ -188,10 +188,13 @@ int bshuf_set_variant(int v) {
     // copy-out at the end of its block's parse (not deferred), 8192 the
     // hand-scheduled re-test chain, 16384 the hand-scheduled search windows,
     // 24576 both, 57344 both with the shortcut (319488: + bit-sliced forward transpose), 40960 the re-test chain with its offset-2 shortcut (the
-    // default for byU16 blocks), 65536 the compiled re-test chain; any of
+    // default for byU16 blocks), 65536 the compiled re-test chain, 172032 /
+    // 450560 the 40960 / 319488 defaults with the search-match hand-off in
+    // asm (search_entry); any of
     // them | kNoPipe (1 << 20): no pipelined encode (launch.h)
     const int vv = v & ~kNoPipe;
-    if (vv != 0 && vv != 2 && vv != 4 && vv != 8 && vv != 16 && vv != 32 && vv != 64 && vv != 128 && vv != 512 && vv != 1024 && vv != 2048 && vv != 4096 && vv != 8192 && vv != 16384 && vv != 24576 && vv != 40960 && vv != 57344 && vv != 65536 && vv != 319488)
+    if (vv != 0 && vv != 2 && vv != 4 && vv != 8 && vv != 16 && vv != 32 && vv != 64 && vv != 128 && vv != 512 && vv != 1024 && vv != 2048 && vv != 4096 && vv != 8192 && vv != 16384 && vv != 24576 && vv != 40960 && vv != 57344 && vv != 65536 && vv != 319488 &&
+        vv != 172032 && vv != 450560)
         return -71;
     t_variant = v;
     return 0;
