@@ -331,11 +331,50 @@ struct EmitBytes {
     }
 };
 
+// Each lane with `mine` copies its literal run of n bytes (1..kLaneRun) from
+// D[sp] to S[dp] (LDS, disjoint; the block D has readable bytes past its end):
+// destination dword t is v_alignbyte of source dwords t and t+1 at one shift
+// for the whole run, so only the head and tail dwords (shared with the
+// token / length / offset bytes around the run) take masked writes -- the
+// whole dwords between go out as plain writes, four per step, with no
+// per-piece mask arithmetic (lane_copy16 recomputes five masks per 16 bytes).
+__device__ __forceinline__ void lane_runs(const lds8* D, int sp, lds8* S, int dp, int n, bool mine) {
+    const int k = dp & 3;
+    const int b = sp - k;  // source byte of destination dword 0's byte 0 (may be < 0: masked off)
+    const uint32_t r = (uint32_t)(b & 3);
+    const lds32* W = (const lds32*)(D + (b & ~3));
+    lds32* O = (lds32*)(S + (dp & ~3));
+    const int nd = ((dp + n + 3) >> 2) - (dp >> 2);  // destination dwords touched
+    if (mine) {
+        const int e = dp + n - 4 * ((dp + n - 1) >> 2);  // bytes of the run in its last dword, 1..4
+        const uint32_t mt = e >= 4 ? ~0u : ((1u << (8 * e)) - 1u);
+        uint32_t mh = ~0u << (8 * k);
+        if (nd == 1) mh &= mt;
+        const uint32_t vh = __builtin_amdgcn_alignbyte(W[1], W[0], r);
+        lds_write_masked(lds_addr((lds8*)O), mh, vh & mh);
+        if (nd > 1) {
+            const uint32_t vt = __builtin_amdgcn_alignbyte(W[nd], W[nd - 1], r);
+            lds_write_masked(lds_addr((lds8*)(O + nd - 1)), mt, vt & mt);
+        }
+    }
+    const int last = mine ? nd - 2 : 0;  // interior dwords 1 .. last
+    for (int t = 1; ballot(t <= last) != 0; t += 4) {
+        if (t <= last) {
+            const uint32_t w0 = W[t], w1 = W[t + 1], w2 = W[t + 2], w3 = W[t + 3], w4 = W[t + 4];
+            O[t] = __builtin_amdgcn_alignbyte(w1, w0, r);
+            if (t + 1 <= last) O[t + 1] = __builtin_amdgcn_alignbyte(w2, w1, r);
+            if (t + 2 <= last) O[t + 2] = __builtin_amdgcn_alignbyte(w3, w2, r);
+            if (t + 3 <= last) O[t + 3] = __builtin_amdgcn_alignbyte(w4, w3, r);
+        }
+    }
+}
+
 // Builds the LZ4 bytes of a parsed block from its descriptors, wave-parallel
 // (lane = sequence; a prefix sum places every sequence): record payload at
 // S[4..), literals from the block D.  The last literal run is sequence ns.
-// Returns the payload size.
-template <class Em>
+// Returns the payload size.  kRuns: literal runs by lane_runs (A/B bit
+// 2097152), else lane_copy16 pieces.
+template <bool kRuns, class Em>
 __device__ __forceinline__ int emit_sequences(const lds8* D, const Em& em, const int n, lds8* S,
                                               const int lane) {
     const int ns = em.ns, la = em.la;
@@ -367,7 +406,9 @@ __device__ __forceinline__ int emit_sequences(const lds8* D, const Em& em, const
         // masked writes); otherwise, and for longer runs, run by run by the wave
         const int lane_max =
             __builtin_popcountll(ballot(lit > 16)) >= kLaneRunMin ? kLaneRun : 16;
-        {
+        if constexpr (kRuns) {
+            lane_runs(D, lsrc, S, lp, lit, lit > 0 && lit <= lane_max);
+        } else {
             const bool mine = lit > 0 && lit <= lane_max;
             for (int d0 = 0; ballot(mine && d0 < lit) != 0; d0 += 16)
                 if (mine && d0 < lit) lane_copy16(D, lsrc + d0, S, lp + d0, min(16, lit - d0));
@@ -883,6 +924,316 @@ __device__ __forceinline__ void search_entry(const int mpos, const int mref, con
         : "scc", "memory");
 }
 
+// The whole parse loop of a byU16 LDS block as ONE hand-scheduled asm block
+// (OPT & 524288): the search windows (search_chain), the undo of a matching
+// window's later inserts, the catch-up and first count window (search_entry)
+// and the re-test chain (retest_chain, with its offset-2 shortcut) jump
+// straight into one another; the compiled code between them (the exits'
+// dispatch, a new search's setup after every re-test miss) cost ~60
+// instructions per search.  Entry 0: search from ip (anchor set); entry 1: the
+// sequence (ip, ref, mc, lit) is found and counted, tail = the a-side window
+// at tb.  The rare cases go back to the caller:
+//   kPcLimit    ip >= mflimitPlusOne after a sequence: last literals (anchor = ip);
+//   kPcPartial  the search from ip reached a window that is not full (window
+//               nwin; vpos / vseq: its probe positions and their bytes);
+//   kPcSlow     re-test with ip - 2 or ip + 3 outside the register window
+//               (anchor = ip; table not touched);
+//   kPcLong     re-test: table updated, candidate c2, the first 256 bytes at
+//               ip all equal (anchor = ip): count on;
+//   kPcEntry    a search match (mpos, mref; later inserts undone) whose
+//               catch-up reaches 64 bytes back or whose count reaches 256.
+// Wait states as in the three blocks it is made of.
+enum { kPcLimit = 0, kPcPartial = 1, kPcSlow = 2, kPcLong = 3, kPcEntry = 4 };
+
+__device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor, int& ref, int& mc, int& lit,
+                                           int& ns, int& tb, int& nwin, int& mpos, int& mref, int& c2,
+                                           uint32_t& tail, uint32_t& dlo, uint32_t& dhi, uint32_t& vseq,
+                                           uint32_t& vpos, const int limit, const int mlimit, const int n,
+                                           const uint32_t desc, const uint32_t lane4d, const uint32_t lane8,
+                                           const uint32_t lanev, const uint32_t pq_off, const uint32_t pq_nxt,
+                                           const uint32_t pq_stp) {
+    int code, t0, t1, t2, t3, t4, keep, qs, qstep;
+    uint64_t ne, bm, sy, sz;
+    uint32_t vh, va, vsh, vad, vm, vd, vold, vlo, vhi, vx1, vnxt, vstep, vcand;
+    uint32_t vn, vy, vz, vd0, vc2, vcb, val, vah, vbl, vbh;
+    asm volatile(
+        "s_mov_b32 %[keep], m0\n\t"
+        "s_cmp_eq_u32 %[entry], 1\n\t"
+        "s_cbranch_scc1 L_top%=\n\t"
+        /* ======== a search from p0 = ip: the first window's bytes */
+        "L_nsrch%=:\n\t"
+        "v_add_u32 %[vh], %[ip], %[lanev]\n\t"
+        "v_min_i32 %[vh], %[n], %[vh]\n\t"
+        "v_and_b32 %[va], -4, %[vh]\n\t"
+        "ds_read_b32 %[vlo], %[va] offset:16384\n\t"
+        "ds_read_b32 %[vhi], %[va] offset:16388\n\t"
+        "v_and_b32 %[vh], 3, %[vh]\n\t"
+        "v_add_u32 %[vpos], %[ip], %[pq_off]\n\t"
+        "v_add_u32 %[vnxt], %[ip], %[pq_nxt]\n\t"
+        "v_mov_b32 %[vstep], %[pq_stp]\n\t"
+        "s_add_u32 %[qs], %[ip], 64\n\t"
+        "s_movk_i32 %[qstep], 0x7f\n\t"
+        "s_mov_b32 %[nwin], 0\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[vh]\n\t"
+        /* ======== full search windows (search_chain) */
+        "L_stop%=:\n\t"
+        "s_cmp_gt_i32 %[qs], %[limit]\n\t"
+        "s_cbranch_scc1 L_spart%=\n\t"
+        "v_mul_lo_u32 %[vh], %[vseq], %[kmul]\n\t"
+        "v_min_i32 %[va], %[n], %[vnxt]\n\t"
+        "s_add_u32 %[qs], %[qs], %[qstep]\n\t"
+        "s_add_u32 %[qstep], %[qstep], 64\n\t"
+        "v_lshrrev_b32 %[vsh], 15, %[vh]\n\t"
+        "v_lshrrev_b32 %[vad], 18, %[vh]\n\t"
+        "v_and_b32 %[vsh], 16, %[vsh]\n\t"
+        "v_and_b32 %[vad], 0x3ffc, %[vad]\n\t"
+        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t"
+        "v_lshlrev_b32 %[vd], %[vsh], %[vpos]\n\t"
+        "v_and_b32 %[vh], -4, %[va]\n\t"
+        "ds_mskor_rtn_b32 %[vold], %[vad], %[vm], %[vd]\n\t"
+        "ds_read_b32 %[vlo], %[vh] offset:16384\n\t"
+        "ds_read_b32 %[vhi], %[vh] offset:16388\n\t"
+        "v_and_b32 %[va], 3, %[va]\n\t"
+        "s_waitcnt lgkmcnt(2)\n\t"
+        "v_lshrrev_b32 %[vcand], %[vsh], %[vold]\n\t"
+        "v_bfe_u32 %[vm], %[vold], %[vsh], 2\n\t"
+        "v_and_b32 %[vd], 0xfffc, %[vcand]\n\t"
+        "ds_read_b32 %[vold], %[vd] offset:16384\n\t"
+        "ds_read_b32 %[vx1], %[vd] offset:16388\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_alignbyte_b32 %[vold], %[vx1], %[vold], %[vm]\n\t"
+        "v_cmp_eq_u32 vcc, %[vold], %[vseq]\n\t"
+        "s_cbranch_vccnz L_smatch%=\n\t"
+        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[va]\n\t"
+        "v_mov_b32 %[vpos], %[vnxt]\n\t"
+        "v_add_u32 %[vnxt], %[vnxt], %[vstep]\n\t"
+        "v_add_u32 %[vstep], 64, %[vstep]\n\t"
+        "s_add_u32 %[nwin], %[nwin], 1\n\t"
+        "s_branch L_stop%=\n\t"
+        /* ======== a match at lane js: later lanes whose found entry is
+           <= mpos put it back (positions after the match were never inserted) */
+        "L_smatch%=:\n\t"
+        "s_ff1_i32_b64 %[t0], vcc\n\t"
+        "v_and_b32 %[vd], 0xffff, %[vcand]\n\t"
+        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t"
+        "v_lshlrev_b32 %[vx1], %[vsh], %[vd]\n\t"
+        "v_readlane_b32 %[mpos], %[vpos], %[t0]\n\t"
+        "v_readlane_b32 %[mref], %[vd], %[t0]\n\t"
+        "s_lshl_b64 %[sy], -2, %[t0]\n\t"
+        "v_cmp_ge_u32 %[sz], %[mpos], %[vd]\n\t"
+        "s_and_b64 %[sy], %[sy], %[sz]\n\t"
+        "s_and_saveexec_b64 %[sz], %[sy]\n\t"
+        "ds_mskor_b32 %[vad], %[vm], %[vx1]\n\t"
+        "s_mov_b64 exec, %[sz]\n\t"
+        /* ======== catch-up (64 bytes back) and the first count window from
+           mpos, one LDS round trip (search_entry) */
+        "s_and_b32 %[t0], %[mpos], -4\n\t"
+        "s_and_b32 %[t1], %[mref], -4\n\t"
+        "v_add_u32 %[vx1], %[t0], %[lane4d]\n\t"
+        "v_add_u32 %[vbh], %[t1], %[lane4d]\n\t"
+        "s_add_u32 %[t2], %[mpos], -1\n\t"
+        "s_add_u32 %[t3], %[mref], -1\n\t"
+        "ds_read_b32 %[val], %[vx1]\n\t"
+        "ds_read_b32 %[vah], %[vx1] offset:4\n\t"
+        "ds_read_b32 %[vbl], %[vbh]\n\t"
+        "ds_read_b32 %[vbh], %[vbh] offset:4\n\t"
+        "v_sub_u32 %[vy], %[t2], %[lanev]\n\t"
+        "v_sub_u32 %[vz], %[t3], %[lanev]\n\t"
+        "v_max_i32 %[vn], 0, %[vy]\n\t"
+        "v_max_i32 %[vd0], 0, %[vz]\n\t"
+        "ds_read_u8 %[vn], %[vn] offset:16384\n\t"
+        "ds_read_u8 %[vd0], %[vd0] offset:16384\n\t"
+        "s_and_b32 %[t0], %[mpos], 3\n\t"
+        "s_and_b32 %[t1], %[mref], 3\n\t"
+        "s_sub_u32 %[t2], %[mlimit], %[mpos]\n\t"
+        "s_max_i32 %[t2], %[t2], 0\n\t"
+        "s_waitcnt lgkmcnt(2)\n\t"
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t0]\n\t"
+        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t1]\n\t"
+        "v_xor_b32 %[vx1], %[tail], %[vbl]\n\t"
+        "v_cmp_ne_u32 %[ne], %[tail], %[vbl]\n\t"
+        "v_cmp_le_i32 %[sy], %[anchor], %[vy]\n\t"
+        "v_cmp_le_i32 %[sz], 0, %[vz]\n\t"
+        "s_ff1_i32_b64 %[t3], %[ne]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readlane_b32 %[t4], %[vx1], %[t3]\n\t"
+        "v_cmp_eq_u32 %[bm], %[vn], %[vd0]\n\t"
+        "s_lshl_b32 %[t3], %[t3], 2\n\t"
+        "s_ff1_i32_b32 %[t4], %[t4]\n\t"
+        "s_lshr_b32 %[t4], %[t4], 3\n\t"
+        "s_add_u32 %[t3], %[t3], %[t4]\n\t"
+        "s_cmp_eq_u64 %[ne], 0\n\t"
+        "s_cselect_b32 %[t3], 256, %[t3]\n\t"
+        "s_min_i32 %[t3], %[t3], %[t2]\n\t"
+        "s_and_b64 %[bm], %[bm], %[sy]\n\t"
+        "s_and_b64 %[bm], %[bm], %[sz]\n\t"
+        "s_not_b64 %[bm], %[bm]\n\t"
+        "s_ff1_i32_b64 %[t4], %[bm]\n\t"
+        "s_cmp_lt_i32 %[t4], 0\n\t"
+        "s_cbranch_scc1 L_eslow%=\n\t"
+        "s_cmpk_eq_u32 %[t3], 0x100\n\t"
+        "s_cbranch_scc1 L_eslow%=\n\t"
+        "s_sub_u32 %[ip], %[mpos], %[t4]\n\t"
+        "s_sub_u32 %[ref], %[mref], %[t4]\n\t"
+        "s_add_u32 %[mc], %[t3], %[t4]\n\t"
+        "s_sub_u32 %[mc], %[mc], 4\n\t"
+        "s_sub_u32 %[lit], %[ip], %[anchor]\n\t"
+        "s_mov_b32 %[tb], %[mpos]\n\t"
+        /* ======== the re-test chain (retest_chain) */
+        "L_top%=:\n\t"
+        "s_sub_u32 %[t0], %[ip], %[ref]\n\t"
+        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t"
+        "s_pack_ll_b32_b16 %[t1], %[lit], %[mc]\n\t"
+        "s_and_b32 m0, %[ns], 63\n\t"
+        "s_add_u32 %[ns], %[ns], 1\n\t"
+        "s_add_u32 %[ip], %[ip], %[mc]\n\t"
+        "v_writelane_b32 %[dlo], %[t0], m0\n\t"
+        "v_writelane_b32 %[dhi], %[t1], m0\n\t"
+        "s_and_b32 %[t2], %[ns], 63\n\t"
+        "s_cbranch_scc0 L_flush%=\n\t"
+        "L_flushed%=:\n\t"
+        "s_add_u32 %[ip], %[ip], 4\n\t"
+        "s_mov_b32 %[lit], 0\n\t"
+        "s_cmp_ge_i32 %[ip], %[limit]\n\t"
+        "s_cbranch_scc1 L_lim%=\n\t"
+        "s_sub_u32 %[t0], %[ip], %[tb]\n\t"
+        "s_sub_u32 %[t1], %[t0], 2\n\t"
+        "s_cmp_gt_u32 %[t1], 249\n\t"
+        "s_cbranch_scc1 L_slow%=\n\t"
+        "v_mov_b32_dpp %[vn], %[tail] wave_shl:1 bound_ctrl:0\n\t"
+        "s_and_b32 %[t2], %[t0], 3\n\t"
+        "s_and_b32 %[t3], %[t1], 3\n\t"
+        "s_lshr_b32 %[t0], %[t0], 2\n\t"
+        "v_alignbyte_b32 %[vy], %[vn], %[tail], %[t2]\n\t"
+        "v_alignbyte_b32 %[vz], %[vn], %[tail], %[t3]\n\t"
+        "s_lshr_b32 %[t1], %[t1], 2\n\t"
+        "s_sub_u32 %[t2], %[ip], 2\n\t"
+        "v_readlane_b32 %[t0], %[vy], %[t0]\n\t"
+        "v_readlane_b32 %[t1], %[vz], %[t1]\n\t"
+        "s_cmp_eq_u32 %[t0], %[t1]\n\t"
+        "s_cbranch_scc1 L_p2%=\n\t"
+        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t"
+        "s_mul_i32 %[t1], %[t1], 0x9e3779b1\n\t"
+        "s_lshr_b32 %[t0], %[t0], 18\n\t"
+        "s_lshr_b32 %[t1], %[t1], 18\n\t"
+        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t"
+        "s_and_b32 %[t1], %[t1], 0x3ffe\n\t"
+        "s_and_b32 %[t3], %[ip], -4\n\t"
+        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t"
+        "v_mov_b32 %[vn], %[t1]\n\t"
+        "v_mov_b32 %[vy], %[t2]\n\t"
+        "v_mov_b32 %[vz], %[t0]\n\t"
+        "v_mov_b32 %[vd0], %[ip]\n\t"
+        "ds_read_b32 %[val], %[vcb]\n\t"
+        "ds_read_b32 %[vah], %[vcb] offset:4\n\t"
+        "ds_write_b16 %[vn], %[vy]\n\t"
+        "ds_read_u16 %[vc2], %[vz]\n\t"
+        "ds_write_b16 %[vz], %[vd0]\n\t"
+        "s_and_b32 %[t3], %[ip], 3\n\t"
+        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t"
+        "s_waitcnt lgkmcnt(1)\n\t"
+        "v_and_b32 %[vcb], -4, %[vc2]\n\t"
+        "v_add_u32 %[vcb], %[vcb], %[lane4d]\n\t"
+        "ds_read_b32 %[vbl], %[vcb]\n\t"
+        "ds_read_b32 %[vbh], %[vcb] offset:4\n\t"
+        "v_readfirstlane_b32 %[c2], %[vc2]\n\t"
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t"
+        "s_and_b32 %[t2], %[c2], 3\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t2]\n\t"
+        "L_cmp%=:\n\t"
+        "v_cmp_ne_u32 vcc, %[tail], %[vbl]\n\t"
+        "v_xor_b32 %[vbh], %[tail], %[vbl]\n\t"
+        "s_bitcmp1_b32 vcc_lo, 0\n\t"
+        "s_cbranch_scc1 L_miss%=\n\t"
+        "s_cmp_eq_u64 vcc, 0\n\t"
+        "s_cbranch_scc1 L_long%=\n\t"
+        "s_ff1_i32_b64 %[t0], vcc\n\t"
+        "s_mov_b32 %[ref], %[c2]\n\t"
+        "v_readlane_b32 %[t2], %[vbh], %[t0]\n\t"
+        "s_lshl_b32 %[t0], %[t0], 2\n\t"
+        "s_mov_b32 %[tb], %[ip]\n\t"
+        "s_ff1_i32_b32 %[t2], %[t2]\n\t"
+        "s_lshr_b32 %[t2], %[t2], 3\n\t"
+        "s_add_u32 %[t0], %[t0], %[t2]\n\t"
+        "s_min_i32 %[t0], %[t0], %[t1]\n\t"
+        "s_sub_u32 %[mc], %[t0], 4\n\t"
+        "s_branch L_top%=\n\t"
+        /* a batch of 64 descriptors to LDS (dropped past kDescMax) */
+        "L_flush%=:\n\t"
+        "s_sub_u32 %[t2], %[ns], 64\n\t"
+        "s_cmp_ge_u32 %[t2], 256\n\t"
+        "s_cbranch_scc1 L_flushed%=\n\t"
+        "s_lshl_b32 %[t2], %[t2], 3\n\t"
+        "s_add_u32 %[t2], %[t2], %[desc]\n\t"
+        "v_add_u32 %[vcb], %[t2], %[lane8]\n\t"
+        "ds_write2_b32 %[vcb], %[dlo], %[dhi] offset1:1\n\t"
+        "s_branch L_flushed%=\n\t"
+        /* offset-2 shortcut (retest_chain) */
+        "L_p2%=:\n\t"
+        "s_and_b32 %[t3], %[ip], -4\n\t"
+        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t"
+        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t"
+        "ds_read_b32 %[val], %[vcb]\n\t"
+        "ds_read_b32 %[vah], %[vcb] offset:4\n\t"
+        "s_lshr_b32 %[t0], %[t0], 18\n\t"
+        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t"
+        "v_mov_b32 %[vd0], %[ip]\n\t"
+        "v_mov_b32 %[vz], %[t0]\n\t"
+        "ds_write_b16 %[vz], %[vd0]\n\t"
+        "s_and_b32 %[t3], %[ip], 3\n\t"
+        "s_sub_u32 %[c2], %[ip], 2\n\t"
+        "s_waitcnt lgkmcnt(1)\n\t"
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t"
+        "s_nop 1\n\t"
+        "v_mov_b32_dpp %[vbh], %[tail] wave_shr:1 bound_ctrl:0\n\t"
+        "v_alignbyte_b32 %[vbl], %[tail], %[vbh], 2\n\t"
+        "v_writelane_b32 %[vbl], %[t1], 0\n\t"
+        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t"
+        "s_branch L_cmp%=\n\t"
+        /* ======== a re-test miss: search from anchor + 1 */
+        "L_miss%=:\n\t"
+        "s_mov_b32 %[anchor], %[ip]\n\t"
+        "s_add_u32 %[ip], %[ip], 1\n\t"
+        "s_branch L_nsrch%=\n\t"
+        "L_lim%=:\n\t"
+        "s_mov_b32 %[code], 0\n\t"
+        "s_mov_b32 %[anchor], %[ip]\n\t"
+        "s_branch L_end%=\n\t"
+        "L_spart%=:\n\t"
+        "s_mov_b32 %[code], 1\n\t"
+        "s_branch L_end%=\n\t"
+        "L_slow%=:\n\t"
+        "s_mov_b32 %[code], 2\n\t"
+        "s_mov_b32 %[anchor], %[ip]\n\t"
+        "s_branch L_end%=\n\t"
+        "L_long%=:\n\t"
+        "s_mov_b32 %[code], 3\n\t"
+        "s_mov_b32 %[anchor], %[ip]\n\t"
+        "s_branch L_end%=\n\t"
+        "L_eslow%=:\n\t"
+        "s_mov_b32 %[code], 4\n\t"
+        "L_end%=:\n\t"
+        "s_mov_b32 m0, %[keep]"
+        : [code] "=&s"(code), [ip] "+s"(ip), [anchor] "+s"(anchor), [ref] "+s"(ref), [mc] "+s"(mc),
+          [lit] "+s"(lit), [ns] "+s"(ns), [tb] "+s"(tb), [nwin] "+s"(nwin), [mpos] "+s"(mpos),
+          [mref] "+s"(mref), [c2] "+s"(c2), [t0] "=&s"(t0), [t1] "=&s"(t1), [t2] "=&s"(t2),
+          [t3] "=&s"(t3), [t4] "=&s"(t4), [keep] "=&s"(keep), [qs] "=&s"(qs), [qstep] "=&s"(qstep),
+          [ne] "=&s"(ne), [bm] "=&s"(bm), [sy] "=&s"(sy), [sz] "=&s"(sz), [tail] "+v"(tail),
+          [dlo] "+v"(dlo), [dhi] "+v"(dhi), [vseq] "+v"(vseq), [vpos] "+v"(vpos), [vh] "=&v"(vh),
+          [va] "=&v"(va), [vsh] "=&v"(vsh), [vad] "=&v"(vad), [vm] "=&v"(vm), [vd] "=&v"(vd),
+          [vold] "=&v"(vold), [vlo] "=&v"(vlo), [vhi] "=&v"(vhi), [vx1] "=&v"(vx1), [vnxt] "=&v"(vnxt),
+          [vstep] "=&v"(vstep), [vcand] "=&v"(vcand), [vn] "=&v"(vn), [vy] "=&v"(vy), [vz] "=&v"(vz),
+          [vd0] "=&v"(vd0), [vc2] "=&v"(vc2), [vcb] "=&v"(vcb), [val] "=&v"(val), [vah] "=&v"(vah),
+          [vbl] "=&v"(vbl), [vbh] "=&v"(vbh)
+        : [entry] "s"(entry), [limit] "s"(limit), [mlimit] "s"(mlimit), [n] "s"(n), [desc] "s"(desc),
+          [kmul] "s"(2654435761u), [ffff] "s"(0xFFFFu), [lane4d] "v"(lane4d), [lane8] "v"(lane8),
+          [lanev] "v"(lanev), [pq_off] "v"(pq_off), [pq_nxt] "v"(pq_nxt), [pq_stp] "v"(pq_stp)
+        : "vcc", "scc", "memory");
+    return code;
+}
+
 // Greedy LZ4 parse of D[0..n) with table T (zeroed).  Every sequence goes to
 // em.seq() once its match is final, the trailing literal run to em.last().
 // Returns the compressed size, or -1 when the emitter ran out of descriptor
@@ -901,7 +1252,104 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                                 !std::is_same<Blk, GblBlk>::value;
     // the search-match -> re-test hand-off in one asm block (OPT & 131072)
     constexpr bool kAsmEntry = kAsmRetest && (OPT & 131072) != 0;
+    // the whole loop in one asm block (OPT & 524288, parse_chain)
+    constexpr bool kFused = kAsmRetest && (OPT & 524288) != 0;
     int op = 0, anchor = 0;
+    if constexpr (kFused) {
+        if (n >= kLz4MinLength) {
+            const int limit = n - kMfLimit + 1;  // mflimitPlusOne
+            const int mlimit = n - kLastLiterals;
+            const uint32_t lane4d = (uint32_t)(uintptr_t)D + 4u * (uint32_t)lane;
+            const uint32_t lane8 = 8u * (uint32_t)lane;
+            const uint32_t desc_addr = (uint32_t)(uintptr_t)em.desc;
+            // this lane's probe offsets in a search's first window (probe_lane)
+            const ProbeLane q = probe_lane(lane);
+            const uint32_t pq_off = (uint32_t)(q.off - (lane == 0 ? 1 : 0));
+            const uint32_t pq_nxt = (uint32_t)(q.off + q.step), pq_stp = (uint32_t)(q.step + kWave);
+            int ip = 1, entry = 0, ref = 0, mc = 0, lit = 0, tb = 0, nwin = 0, mpos = 0, mref = 0, c2 = 0;
+            uint32_t tail = 0, vseq = 0, vpos = 0;
+            for (;;) {
+                // every scalar the asm keeps in SGPRs, provably uniform here
+                entry = uni(entry), ip = uni(ip), anchor = uni(anchor), ref = uni(ref), mc = uni(mc);
+                lit = uni(lit), em.ns = uni(em.ns), tb = uni(tb), nwin = uni(nwin), mpos = uni(mpos);
+                mref = uni(mref), c2 = uni(c2);
+                const int code = parse_chain(entry, ip, anchor, ref, mc, lit, em.ns, tb, nwin, mpos, mref, c2,
+                                             tail, em.dlo, em.dhi, vseq, vpos, limit, mlimit, n, desc_addr,
+                                             lane4d, lane8, (uint32_t)lane, pq_off, pq_nxt, pq_stp);
+                if (code == kPcLimit) break;
+                CountOut co;
+                if (code == kPcPartial) {
+                    // the search from p0 = ip reached a window that is not
+                    // full: its valid probes by the general window
+                    const int p0 = ip, k0 = kWave * nwin;
+                    const ProbeLane q1 = probe_lane(k0 + lane + 1);
+                    const bool valid = p0 + q1.off <= limit;
+                    const uint64_t vmask = ballot(valid);
+                    if (vmask == 0) break;
+                    const uint32_t h = hash4(vseq);
+                    const uint32_t cand = T.exchange_if(h, vpos, valid);
+                    const uint32_t dcand = lds_rd32(D, (int)cand);
+                    const uint64_t mm = vmask & ballot(dcand == vseq);
+                    if (!mm) break;
+                    const int js = ffs64(mm);
+                    mpos = __builtin_amdgcn_readlane((int)vpos, js);
+                    if (valid && lane > js && cand <= (uint32_t)mpos) T.put(h, cand);
+                    mref = __builtin_amdgcn_readlane((int)cand, js);
+                    co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
+                } else if (code == kPcEntry) {
+                    co = catch_and_count(D, n, mpos, mref, anchor, mlimit, lane);
+                } else {
+                    // re-test outside the register window (kPcSlow: table ops
+                    // here) or longer than 256 bytes (kPcLong): from the window at ip
+                    if (code == kPcSlow) {
+                        const uint32_t h2 = hash4(lds_rd32(D, ip - 2)), h0 = hash4(lds_rd32(D, ip));
+                        T.put(h2, (uint32_t)(ip - 2));
+                        c2 = uni((int)T.get(h0));
+                        T.put(h0, (uint32_t)ip);
+                    }
+                    uint32_t va = rdw(D, ip + 4 * lane, n), vb = rdw(D, c2 + 4 * lane, n);
+                    uint64_t ne = ballot(va != vb);
+                    if (ne & 1ull) {
+                        entry = 0;  // a miss: search from anchor + 1
+                        ip = anchor + 1;
+                        continue;
+                    }
+                    int total = 0, c;
+                    for (;;) {
+                        c = kWinBytes;
+                        if (ne) {
+                            const int f = ffs64(ne);
+                            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)(va ^ vb), f);
+                            c = 4 * f + (__builtin_ctz(x) >> 3);
+                        }
+                        c = min(c, max(mlimit - (ip + total), 0));
+                        if (c < kWinBytes) break;
+                        total += kWinBytes;
+                        va = rdw(D, ip + total + 4 * lane, n);
+                        vb = rdw(D, c2 + total + 4 * lane, n);
+                        ne = ballot(va != vb);
+                    }
+                    tail = va;
+                    tb = ip + total;
+                    ref = c2;
+                    mc = total + c - kMinMatch;
+                    lit = 0;
+                    entry = 1;
+                    continue;
+                }
+                // a search match (mpos, mref), caught up and counted here
+                ip = mpos - co.back;
+                ref = mref - co.back;
+                mc = co.back + co.cnt;
+                lit = ip - anchor;
+                tb = co.tail_base;
+                tail = co.tail;
+                entry = 1;
+            }
+        }
+        em.last(op, anchor, n);
+        return op;
+    }
     if (n >= kLz4MinLength) {
         const int limit = n - kMfLimit + 1;  // mflimitPlusOne
         const int mlimit = n - kLastLiterals;
@@ -1648,14 +2096,14 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                 // descriptors are buffered in VGPRs
                 using Em = typename std::conditional<(VAR & 8192) != 0, EmitDescV, EmitDesc>::type;
                 Em em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768 | 131072))>(D, n, T, em, lane);
+                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768 | 131072 | 524288))>(D, n, T, em, lane);
                 KSTAMP(1);
                 if (em.ns > kDescMax) c = -1;  // more sequences than descriptor slots
                 if (c >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     lds8* S = L0;
-                    c = emit_sequences(D, em, n, S, lane);
+                    c = emit_sequences<(VAR & 2097152) != 0>(D, em, n, S, lane);
                     if (lane < 4) S[lane] = (uint8_t)((uint32_t)c >> (24 - 8 * lane));
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -1970,6 +2418,12 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         if (v == 172032) return launch_enc_t<EK, WIDE, VAR | 172032>(a, nb, lds, s);
         if (v == 450560 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 450560>(a, nb, lds, s);
         if (v == 450560) return launch_enc_t<EK, WIDE, VAR | 172032>(a, nb, lds, s);
+        // + the whole parse loop as one asm block (parse_chain, | 524288)
+        if (v == 974848 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 974848>(a, nb, lds, s);
+        if (v == 974848 || v == 696320) return launch_enc_t<EK, WIDE, VAR | 696320>(a, nb, lds, s);
+        // + literal runs by lane_runs in the emission (| 2097152)
+        if (v == 3072000 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 3072000>(a, nb, lds, s);
+        if (v == 3072000 || v == 2793472) return launch_enc_t<EK, WIDE, VAR | 2793472>(a, nb, lds, s);
         if (v == 319488 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 319488>(a, nb, lds, s);
         if (v == 319488) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
     }

@@ -190,11 +190,14 @@ int bshuf_set_variant(int v) {
     // 24576 both, 57344 both with the shortcut (319488: + bit-sliced forward transpose), 40960 the re-test chain with its offset-2 shortcut (the
     // default for byU16 blocks), 65536 the compiled re-test chain, 172032 /
     // 450560 the 40960 / 319488 defaults with the search-match hand-off in
-    // asm (search_entry); any of
+    // asm (search_entry), 696320 / 974848 the same with the whole parse loop
+    // as one asm block (parse_chain), 2793472 / 3072000 those with the
+    // emission's literal runs by lane_runs; any of
     // them | kNoPipe (1 << 20): no pipelined encode (launch.h)
     const int vv = v & ~kNoPipe;
     if (vv != 0 && vv != 2 && vv != 4 && vv != 8 && vv != 16 && vv != 32 && vv != 64 && vv != 128 && vv != 512 && vv != 1024 && vv != 2048 && vv != 4096 && vv != 8192 && vv != 16384 && vv != 24576 && vv != 40960 && vv != 57344 && vv != 65536 && vv != 319488 &&
-        vv != 172032 && vv != 450560)
+        vv != 172032 && vv != 450560 && vv != 696320 && vv != 974848 &&
+        vv != 2793472 && vv != 3072000)
         return -71;
     t_variant = v;
     return 0;

@@ -164,7 +164,7 @@ def test_variant_knob_rejects_ablations(bs):
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960, 57344, 65536, 319488, 172032, 450560])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960, 57344, 65536, 319488, 172032, 450560, 696320, 974848, 2793472, 3072000])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
@@ -199,7 +199,7 @@ def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     _with_variant(bs, variant, run)
 
 
-@pytest.mark.parametrize("variant", [8192, 16384, 24576, 40960, 57344, 65536, 319488, 172032, 450560])
+@pytest.mark.parametrize("variant", [8192, 16384, 24576, 40960, 57344, 65536, 319488, 172032, 450560, 696320, 974848, 2793472, 3072000])
 def test_encoder_variant_all_element_sizes(bs, oracle, variant):
     """A variant that applies to every element size (8192: the hand-scheduled
     re-test chain) on the oracle matrix of test_lz4_matches_oracle plus the
