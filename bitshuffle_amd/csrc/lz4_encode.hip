@@ -2410,20 +2410,22 @@ hipError_t launch_enc_t(const EncArgs& a, int64_t nb, size_t lds, hipStream_t s)
         // ... and the search-match -> re-test hand-off in asm (search_entry,
         // | 131072): k_lz4_encode 2 GiB G1 0.677 -> 0.631 ms, 1 GiB G2 0.911
         // -> 0.846, 1 GiB as E = 3 1.347 -> 1.218, E = 12 1.229 -> 1.133 per
-        // launch (profiles/r05/r5b); 319488 / 40960 stay as A/B variants
-        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 172032 : 450560)>(a, nb, lds, s);
+        // launch (profiles/r05/r5b)
+        // ... and the whole parse loop as one asm block (parse_chain, |
+        // 524288) with the emission's literal runs by lane_runs (| 2097152):
+        // 2 GiB G1 0.621 -> 0.592 ms, 1 GiB G2 0.832 -> 0.781, E = 3 1.213 ->
+        // 1.036, E = 12 1.129 -> 1.001 per launch (profiles/r05/r5d; lane_runs
+        // alone -0.3..-0.6 % of that); 450560 / 172032, 319488 / 40960 stay as
+        // A/B variants
+        if (v == 0) return launch_enc_t<EK, WIDE, VAR | (EK == 0 ? 2793472 : 3072000)>(a, nb, lds, s);
+        if (v == 3072000 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 3072000>(a, nb, lds, s);
+        if (v == 3072000 || v == 2793472) return launch_enc_t<EK, WIDE, VAR | 2793472>(a, nb, lds, s);
         if (v == 40960) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
         if (v == 57344) return launch_enc_t<EK, WIDE, VAR | 57344>(a, nb, lds, s);
-        // + the search-match -> re-test hand-off in asm (search_entry)
+        // the search-match -> re-test hand-off in asm (search_entry), compiled glue
         if (v == 172032) return launch_enc_t<EK, WIDE, VAR | 172032>(a, nb, lds, s);
         if (v == 450560 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 450560>(a, nb, lds, s);
         if (v == 450560) return launch_enc_t<EK, WIDE, VAR | 172032>(a, nb, lds, s);
-        // + the whole parse loop as one asm block (parse_chain, | 524288)
-        if (v == 974848 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 974848>(a, nb, lds, s);
-        if (v == 974848 || v == 696320) return launch_enc_t<EK, WIDE, VAR | 696320>(a, nb, lds, s);
-        // + literal runs by lane_runs in the emission (| 2097152)
-        if (v == 3072000 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 3072000>(a, nb, lds, s);
-        if (v == 3072000 || v == 2793472) return launch_enc_t<EK, WIDE, VAR | 2793472>(a, nb, lds, s);
         if (v == 319488 && EK != 0) return launch_enc_t<EK, WIDE, VAR | 319488>(a, nb, lds, s);
         if (v == 319488) return launch_enc_t<EK, WIDE, VAR | 40960>(a, nb, lds, s);
     }

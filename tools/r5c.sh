@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 call c: full GPU suite at the new defaults, bench config 2 + modes,
-# encoder / decoder diag splits, host path (config 5 + host C-ABI).
+# encoder / decoder diag splits.
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
 bash tools/gpu_step.sh r5c \
  "600:python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider" \
@@ -10,5 +10,4 @@ bash tools/gpu_step.sh r5c \
  "200:python -u tools/diag_encode.py 1 1 3" \
  "200:python -u tools/diag_encode.py 1 2" \
  "200:python -u tools/diag_decode.py 1 1" \
- "200:python -u tools/diag_decode.py 1 2" \
- "900:bash tools/h5_bench.sh r5c"
+ "200:python -u tools/diag_decode.py 1 2"
