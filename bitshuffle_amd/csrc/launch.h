@@ -45,8 +45,6 @@ constexpr int kPipeSegs = 8;
 constexpr int64_t kPipeMinBlocks = 65536;  // shorter calls run unsegmented
 constexpr int kPipeEvents = kPipeSegs + 2;  // fork, one per segment, join
 constexpr int kNoPipe = 1 << 20;  // no pipelined encode
-constexpr int kDecAlt = 1 << 22;  // the decoder's A/B alternative (lz4_decode.hip)
-bool dec_alt();
 struct PipeCtx {
     hipStream_t side = nullptr;
     hipEvent_t ev[kPipeEvents] = {};

@@ -560,106 +560,11 @@ __device__ __forceinline__ int read_ext(const Src& Cb, int& q, uint64_t w, int a
     }
 }
 
-// The matches of one 64-sequence step (lane = sequence; mm: lanes with a
-// match), in batches of mutually independent sequences as in lz4_exec_block,
-// but a batch's matches run TOGETHER as one list of destination dwords
-// ("units"), 64 per pass: unit t of a match is its aligned destination dword
-// w, written under the mask of the match's bytes in it (plain write when
-// whole).  Its value is one v_perm of the source dword x = the 4 bytes at a:
-//   copy (off >= ml):         a = w - off, bytes in order;
-//   period off in {1, 2, 4}:  a = mop - off (the pattern, final before the
-//                             match), byte b = x[(w + b - mop) mod off];
-//   off 0:                    zeros (LZ4_write32(op, 0), lz4/lz4.c:501).
-// Every source byte a unit uses is final before its batch (the batch rule),
-// so a pass's reads may precede its writes; dwords shared by two matches take
-// masked writes from two lanes of one instruction, which both land.  Other
-// periods (off 3, 5, 6, ... < ml; rare) run one after another by the wave.
-// A lane finds its unit's match among the batch's few matches by compares
-// against their unit offsets (an exclusive prefix over the step).
-template <class DG>
-__device__ __forceinline__ void match_units(lds8* D, const int mop, const int off, const int ml,
-                                            const int rend, const uint64_t mm, const int lane, DG& dg) {
-    const bool per = off < ml;
-    const bool gpl = per && off != 0 && off != 1 && off != 2 && off != 4;
-    const uint64_t gp = mm & ballot(gpl);
-    const int nu = (ml > 0 && !gpl) ? ((mop + ml - 1) >> 2) - (mop >> 2) + 1 : 0;
-    const int uinc = wave_incl_sum(nu, lane);
-    const int uex = uinc - nu;
-    // what a unit's lane needs of its match: dword address base, byte range,
-    // source (bit 0: relative to w), v_perm selector
-    const int wb = 4 * ((mop >> 2) - uex);
-    const int mend = mop + ml;
-    const int sax = per ? 2 * (mop - off) : 2 * (-off) + 1;
-    // byte b of a periodic unit is pattern byte (b + r) mod off, r = (w - mop) mod 4
-    const int r = (-mop) & 3;
-    const uint32_t sel = !per      ? 0x03020100u
-                       : off == 0  ? 0x0C0C0C0Cu  // v_perm selector 12: byte 0x00
-                       : off == 1  ? 0u
-                       : off == 2  ? ((r & 1) ? 0x00010001u : 0x01000100u)
-                                   : __builtin_amdgcn_alignbyte(0x03020100u, 0x03020100u, (uint32_t)r);
-    const lds32* W = (const lds32*)D;
-    uint64_t todo = mm;
-    while (todo) {
-        const int f = ffs64(todo);
-        const int opf = __builtin_amdgcn_readlane(mop, f);
-        const uint64_t above = ~((2ull << f) - 1ull);  // lanes > f (none for f = 63)
-        const uint64_t sm = ballot(rend > opf) & mm & above;
-        const uint64_t batch = todo & (sm ? (1ull << ffs64(sm)) - 1ull : ~0ull);
-        const uint64_t sb = batch & ~gp;
-        dg.count(1, 1);
-        if (sb) {
-            const int u0 = __builtin_amdgcn_readlane(uex, ffs64(sb));
-            const int u1 = __builtin_amdgcn_readlane(uinc, 63 - __builtin_clzll(sb));
-            for (int t0 = u0; t0 < u1; t0 += kWave) {
-                const int t = t0 + lane;
-                int o_wb = 0, o_mop = 0, o_end = 0, o_sax = 0;
-                uint32_t o_sel = 0;
-                for (uint64_t b = sb; b; b &= b - 1) {
-                    const int l = ffs64(b);
-                    if (__builtin_amdgcn_readlane(uinc, l) <= t0) continue;  // ends before this pass
-                    if (__builtin_amdgcn_readlane(uex, l) >= t0 + kWave) break;  // and all later ones start after it
-                    if (t >= __builtin_amdgcn_readlane(uex, l)) {
-                        o_wb = __builtin_amdgcn_readlane(wb, l);
-                        o_mop = __builtin_amdgcn_readlane(mop, l);
-                        o_end = __builtin_amdgcn_readlane(mend, l);
-                        o_sax = __builtin_amdgcn_readlane(sax, l);
-                        o_sel = (uint32_t)__builtin_amdgcn_readlane((int)sel, l);
-                    }
-                }
-                if (t < u1) {
-                    const int w = o_wb + 4 * t;
-                    const int a = ((o_sax & 1) ? w : 0) + (o_sax >> 1);  // >= -3
-                    const int al = a & ~3;
-                    const uint32_t x0 = W[max(al, 0) >> 2], x1 = W[(al >> 2) + 1];
-                    const uint32_t x = __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)(a & 3));
-                    const uint32_t v = __builtin_amdgcn_perm(x, x, o_sel);
-                    const uint32_t m = low_bytes_mask(o_end - w) & ~low_bytes_mask(o_mop - w);
-                    if (m == ~0u) {
-                        ((lds32*)D)[w >> 2] = v;
-                    } else {
-                        lds_write_masked((uint32_t)(uintptr_t)(D + w), m, v & m);
-                    }
-                }
-            }
-        }
-        for (uint64_t cm = batch & gp; cm; cm &= cm - 1) {
-            const int l = ffs64(cm);
-            dg.count(2, 1);
-            wave_match(D, __builtin_amdgcn_readlane(mop, l), __builtin_amdgcn_readlane(off, l),
-                       __builtin_amdgcn_readlane(ml, l), lane);
-        }
-        todo &= ~batch;
-    }
-}
-
 // Phase 2 for one block.  The record payload starts at byte cp of the
 // 4-aligned LDS buffer Cb; pos[0..nseq) are its token positions (payload-
 // relative, validated by the scan); pos0 is this lane's prefetched pos[lane].
 // dg: the diagnostic build's phase clock (fields, literals, matches).
-// kSeg: every match of a batch except general-period ones (off < ml, off not
-// 0 / 1 / 2 / 4) as one segmented dword pass (match_units); else short
-// non-overlapping matches per lane and the rest one after another by the wave.
-template <bool kInPlace = false, int ABL = 0, bool kSeg = false, class Src>
+template <bool kInPlace = false, int ABL = 0, class Src>
 __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8* D,
                                const uint32_t* __restrict__ pos, const int nseq, uint32_t pos0,
                                const int lane, DDiag& dg) {
@@ -744,11 +649,6 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
         const int mop = op + lit;
         const int rend = mop - off + min(ml, off);
         const uint64_t mm = (ABL & 2) ? 0ull : ballot(ml > 0);
-        if constexpr (kSeg) {
-            match_units(D, mop, off, ml, rend, mm, lane, dg);
-            dg.stamp(2);
-            continue;
-        }
         const uint64_t cmask = mm & (ballot(ml > 16) | ballot(off < ml));  // only the head can overlap itself
         uint64_t todo = mm;
         while (todo) {
@@ -1201,8 +1101,6 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
     // One ~8.9 KiB buffer per wave: every record read is an LDS read and the
     // occupancy of the global-read decoder stays.
     constexpr bool kIP = (VAR & 512) != 0;
-    // VAR & 4096: a batch's matches as one segmented dword pass (match_units)
-    constexpr bool kSeg = (VAR & 4096) != 0;
     auto cbuf_of = [&](const Span& sp) -> lds8* {
         return kIP ? to_lds(smem) + a.ip_end - 16 * span_chunks(a, sp) : Cbuf;
     };
@@ -1265,20 +1163,20 @@ void k_lz4_decode(DecArgs a, int64_t nb) {
             const uintptr_t b0 = (uintptr_t)(rec + 4);
             const GblRec src{b0, (b0 + (uintptr_t)clen - 1) & ~(uintptr_t)3};
             if (!(VAR & 64))
-                lz4_exec_block<false, 0, kSeg>(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane, dg);
+                lz4_exec_block(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane, dg);
         } else {
             clen = (int)(((uint32_t)C[0] << 24) | ((uint32_t)C[1] << 16) | ((uint32_t)C[2] << 8) | C[3]);
             const int mx = (int)((cur.scan >> 32) & 0xFFFF) - kMxBias;
             if (!kIP || mx <= (int)(CB - D) + cp + 4) {
                 if (!(VAR & 64))
-                    lz4_exec_block<kIP, (VAR >> 10) & 3, kSeg>(LdsRec{CB}, cp + 4, D, cur.loc.seq + cur.o0 / 3,
+                    lz4_exec_block<kIP, (VAR >> 10) & 3>(LdsRec{CB}, cp + 4, D, cur.loc.seq + cur.o0 / 3,
                                         (int)cur.scan, cur_pos, lane, dg);
             } else {
                 // too little room to decode in place: the record from L2
                 const uintptr_t b0 = (uintptr_t)(cur.loc.in + cur.o0 + 4);
                 const GblRec src{b0, (b0 + (uintptr_t)clen - 1) & ~(uintptr_t)3};
                 if (!(VAR & 64))
-                    lz4_exec_block<false, 0, kSeg>(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane, dg);
+                    lz4_exec_block(src, 0, D, cur.loc.seq + cur.o0 / 3, (int)cur.scan, cur_pos, lane, dg);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1758,15 +1656,11 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
         a.stage_off = 0;
     }
     const void* fn = nullptr;
-    // bshuf_set_variant(v | kDecAlt): the in-place decoder's alternative
-    // (A/B): segmented match batches
-    const int ipv = dec_alt() ? 512 | 4096 : 512;
 #define BSHUF_DEC(ekv, v) reinterpret_cast<const void*>(k_lz4_decode<ekv, v>)
-#define BSHUF_DEC_IP(ekv) (ipv == 512 ? BSHUF_DEC(ekv, 512) : BSHUF_DEC(ekv, 4608))
     switch (ek) {
-        case 1: fn = inplace ? BSHUF_DEC_IP(1) : touch ? BSHUF_DEC(1, 48) : (grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0)); break;
+        case 1: fn = inplace ? BSHUF_DEC(1, 512) : touch ? BSHUF_DEC(1, 48) : (grec ? BSHUF_DEC(1, 16) : BSHUF_DEC(1, 0)); break;
         case 2:
-            fn = inplace ? BSHUF_DEC_IP(2) : touch ? BSHUF_DEC(2, 48) : (grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0));
+            fn = inplace ? BSHUF_DEC(2, 512) : touch ? BSHUF_DEC(2, 48) : (grec ? BSHUF_DEC(2, 16) : BSHUF_DEC(2, 0));
 #ifdef BSHUF_DIAG
             // diagnostic build only -- ABLATIONS for timing, wrong output:
             // 8 no output stores, 64 no sequence execution
@@ -1778,17 +1672,16 @@ hipError_t decode_impl(DecArgs& a, int64_t nb, bool aligned, hipStream_t s) {
 #endif
             break;
         case 4:
-            fn = inplace ? BSHUF_DEC_IP(4) : touch ? BSHUF_DEC(4, 48) : (grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0));
+            fn = inplace ? BSHUF_DEC(4, 512) : touch ? BSHUF_DEC(4, 48) : (grec ? BSHUF_DEC(4, 16) : BSHUF_DEC(4, 0));
 #ifdef BSHUF_DIAG
             if (diag_variant() == 8) fn = BSHUF_DEC(4, 520);
             if (diag_variant() == 64) fn = BSHUF_DEC(4, 576);
             if (diag_variant() == 72) fn = BSHUF_DEC(4, 584);
 #endif
             break;
-        case 8: fn = inplace ? BSHUF_DEC_IP(8) : touch ? BSHUF_DEC(8, 48) : (grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0)); break;
-        default: fn = inplace ? BSHUF_DEC_IP(0) : touch ? BSHUF_DEC(0, 48) : (grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0)); break;
+        case 8: fn = inplace ? BSHUF_DEC(8, 512) : touch ? BSHUF_DEC(8, 48) : (grec ? BSHUF_DEC(8, 16) : BSHUF_DEC(8, 0)); break;
+        default: fn = inplace ? BSHUF_DEC(0, 512) : touch ? BSHUF_DEC(0, 48) : (grec ? BSHUF_DEC(0, 16) : BSHUF_DEC(0, 0)); break;
     }
-#undef BSHUF_DEC_IP
 #undef BSHUF_DEC
     hipError_t e = hipSuccess;
 #if defined(BSHUF_DIAG) || defined(BSHUF_OCC)

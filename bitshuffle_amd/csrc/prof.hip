@@ -59,8 +59,7 @@ bool prof_on() { return P().on; }
 // A/B knob: per calling thread, and only byte-identical variants are accepted
 // (the timing ablations that change the output exist in the diag build only).
 static thread_local int t_variant = 0;
-int tuning_variant() { return t_variant & ~(kNoPipe | kDecAlt); }
-bool dec_alt() { return (t_variant & kDecAlt) != 0; }
+int tuning_variant() { return t_variant & ~kNoPipe; }
 
 namespace {
 // The calling thread's side streams, one per device (kept for the thread's
@@ -194,9 +193,8 @@ int bshuf_set_variant(int v) {
     // (search_entry), 2793472 / 3072000 (the defaults) those with the whole
     // parse loop as one asm block (parse_chain) and the emission's literal
     // runs by lane_runs; any of
-    // them | kNoPipe (1 << 20): no pipelined encode, | kDecAlt (1 << 22): the
-    // decoder's alternative (launch.h)
-    const int vv = v & ~(kNoPipe | kDecAlt);
+    // them | kNoPipe (1 << 20): no pipelined encode (launch.h)
+    const int vv = v & ~kNoPipe;
     if (vv != 0 && vv != 2 && vv != 4 && vv != 8 && vv != 16 && vv != 32 && vv != 64 && vv != 128 && vv != 512 && vv != 1024 && vv != 2048 && vv != 4096 && vv != 8192 && vv != 16384 && vv != 24576 && vv != 40960 && vv != 57344 && vv != 65536 && vv != 319488 &&
         vv != 172032 && vv != 450560 &&
         vv != 2793472 && vv != 3072000)

@@ -164,7 +164,7 @@ def test_variant_knob_rejects_ablations(bs):
     assert bs.lib.bshuf_set_variant(0) == 0
 
 
-@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960, 57344, 65536, 319488, 172032, 450560, 2793472, 3072000, 1 << 22])
+@pytest.mark.parametrize("variant", [128, 2, 4, 8, 16, 32, 64, 512, 2048, 4096, 8192, 16384, 24576, 40960, 57344, 65536, 319488, 172032, 450560, 2793472, 3072000])
 def test_encoder_alternate_paths_match_oracle(bs, oracle, variant):
     """Byte-identical alternate paths (elem_size 2): 128 the insert/
     read-back search window (the fallback when the LDS-atomic lane-order
@@ -293,14 +293,13 @@ def _crafted_block(rng, n, oracle):
         return bytes(pay)
 
 
-@pytest.mark.parametrize("variant", [0, 1 << 22])
 @pytest.mark.parametrize("E", [1, 4])
-def test_decoder_crafted_sequences_match_oracle(bs, oracle, variant, E):
+def test_decoder_crafted_sequences_match_oracle(bs, oracle, E):
     """Streams of hand-built LZ4 records (not what the encoder emits): every
     decoder match path -- per-lane and wave copies, periods 0/1/2/3/4/other,
     matches reading the previous sequence's output (batch breaks), long
-    lengths -- against the oracle's LZ4_decompress_safe restatement, default
-    decoder and its alternative (1 << 22: segmented match batches)."""
+    lengths -- against the oracle's LZ4_decompress_safe restatement.  Blocks
+    whose in-place margin fails take the decoder's global-record path."""
     rng = np.random.default_rng(4242 + E)
     nbytes = 8192
     frames = bytearray()
@@ -311,10 +310,8 @@ def test_decoder_crafted_sequences_match_oracle(bs, oracle, variant, E):
     shape, dt = (40 * nbytes // E,), DTYPES[E]
     want = oracle.decompress_lz4(buf, shape, dt, nbytes // E)
 
-    def run():
-        got = bs.decompress_lz4(buf, shape, dt, nbytes // E)
-        assert got.tobytes() == want.tobytes()
-    _with_variant(bs, variant, run)
+    got = bs.decompress_lz4(buf, shape, dt, nbytes // E)
+    assert got.tobytes() == want.tobytes()
 
 
 def _record(payload):
