@@ -37,6 +37,7 @@ PROTOTYPES = {
     "bshuf_decompress_lz4_dev": (_i64, [_vp, _sz, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp, _vp]),
     "bshuf_decompress_lz4_dev_dlen": (_i64, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp,
                                              _vp]),
+    "bshuf_lz4_block_index_dev": (_i64, [_vp, _sz, _sz, _sz, _sz, _vp, _sz, _vp, _vp, _vp]),
     "bshuf_compress_lz4_batch_dev_workspace": (_sz, [_vp, _sz, _sz, _sz]),
     "bshuf_compress_lz4_batch_dev": (_i64, [_vp, _vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _vp, _vp]),
     "bshuf_decompress_lz4_batch_dev_workspace": (_sz, [_vp, _vp, _sz, _sz, _sz]),

@@ -234,6 +234,27 @@ def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None
     return out
 
 
+def block_index_dev(buf, size, elem_size, block_size=0, workspace=None, stream=None):
+    """The block index of the framed stream in uint8 device tensor `buf` for
+    `size` elements of `elem_size` bytes (bshuf_lz4_block_index_dev, the
+    decoder's parallel header walk): an int64 tensor of every block's byte
+    offset.  Raises BshufError(-91) when the records do not tile the stream,
+    -1001 when a block cannot be placed."""
+    torch = _torch()
+    nb = int(lib.bshuf_lz4_dev_nblocks(size, elem_size, block_size))
+    offs = torch.empty(max(nb, 1), dtype=torch.int64, device=buf.device)
+    status = torch.empty(1, dtype=torch.int64, device=buf.device)
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    wsb = workspace.numel() if workspace is not None else 0
+    _check(lib.bshuf_lz4_block_index_dev(_dptr(buf), buf.numel(), size, elem_size, block_size, ws,
+                                         wsb, _dptr(offs), _dptr(status), _stream(stream)))
+    if int(status.item()) != 0:
+        _fail(-91)
+    if nb and bool((offs[:nb] == -1).any()):
+        _fail(-1001)  # a block the walk could not place (the decoder's code for it)
+    return offs[:nb]
+
+
 def _ptr_array(vals):
     arr = (ctypes.c_void_p * len(vals))(*[ctypes.c_void_p(v) for v in vals])
     return ctypes.cast(arr, ctypes.c_void_p), arr

@@ -312,6 +312,45 @@ int64_t bshuf_decompress_lz4_dev_dlen(const void* in, const int64_t* d_in_nbytes
                           ws_bytes, d_result, block_offsets, stream);
 }
 
+// The block index of a framed stream alone (K6, the decoder's parallel
+// header walk): block k's byte offset in `in`, for callers that split one
+// stream's decode across devices (bitshuffle_amd/split.py).  *d_status: 0 when
+// the records tile the stream exactly, else the index's error word (the
+// decoder would return -91); a block the walk could not place holds ~0.
+// Replaces the reference's serial header walk (src/iochain.c:42-64 inside
+// bshuf_blocked_wrap_fun, src/bitshuffle_core.c:1877-1931) when run alone.
+int64_t bshuf_lz4_block_index_dev(const void* in, size_t in_nbytes, size_t size, size_t elem_size,
+                                  size_t block_size, void* ws, size_t ws_bytes,
+                                  uint64_t* block_offsets, int64_t* d_status, void* stream) {
+    Plan p;
+    const int64_t r = make_plan(size, elem_size, block_size, p);
+    if (r) return r;
+    if (!block_offsets || !d_status) return kErrUnsupported;
+    if (!have_device()) return kErrHip;
+    hipStream_t s = (hipStream_t)stream;
+    int64_t cb = (int64_t)in_nbytes - p.tail;
+    if (cb < 0) cb = 0;
+    const size_t need = dec_ws(p, cb, (int64_t)in_nbytes, true, nullptr, nullptr);
+    DevBuf own;
+    if (!ws) {
+        if (own.alloc(need, s) != hipSuccess) return -1;
+        ws = own.p;
+    } else if (ws_bytes < need || ((uintptr_t)ws & 255)) {
+        return kErrUnsupported;
+    }
+    DecodeBufs b;
+    dec_ws(p, cb, (int64_t)in_nbytes, true, &b, (uint8_t*)ws);
+    if (launch_index((const uint8_t*)in, cb, p.L, b, s, nullptr, (int64_t)in_nbytes, p.tail) !=
+        hipSuccess)
+        return kErrHip;
+    if (p.nb && hipMemcpyAsync(block_offsets, b.offs, (size_t)p.nb * 8, hipMemcpyDeviceToDevice, s) !=
+                    hipSuccess)
+        return kErrHip;
+    if (hipMemcpyAsync(d_status, b.idx_err, 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return kErrHip;
+    return 0;
+}
+
 // ---------------------------------------------------------------------------
 // batched device entry points: `count` independent streams per launch
 // ---------------------------------------------------------------------------

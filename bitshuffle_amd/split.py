@@ -10,7 +10,10 @@ concatenated in rank order, ARE the single stream of the whole input, byte for
 byte.  The only exchange is one all-gather of the per-rank compressed byte
 counts; its exclusive scan is each rank's offset in the stream.  Decoding runs
 the same way backwards: rank r decodes bytes [offset_r, offset_r + length_r)
-as a stream of its own shard's size.
+as a stream of its own shard's size.  A stream whose piece boundaries were
+not kept (read back from a file, say) is split with its block index
+(`piece_ranges` over `block_index_dev`, the decoder's parallel header walk
+alone): rank r's piece starts at its first block's offset.
 
 `shard_bounds` splits the blocks as evenly as possible; the last rank also
 takes the partial block and the tail (the reference's layout puts them at the
@@ -25,7 +28,7 @@ RCCL (backend "nccl") for device tensors, gloo on the CPU.
 from .api import default_block_size
 
 __all__ = ["shard_bounds", "stream_offsets", "compress_lz4_split", "decompress_lz4_split",
-           "gather_stream"]
+           "gather_stream", "piece_ranges", "split_stream"]
 
 
 def shard_bounds(size, elem_size, world, block_size=0):
@@ -141,3 +144,33 @@ def gather_stream(piece, lengths, dst=0, group=None):
         return None
     allb = allb.cpu()
     return torch.cat([allb[r * mx: r * mx + lengths[r]] for r in range(world)])
+
+
+def piece_ranges(block_offsets, bounds, stream_len, elem_size, block_size=0):
+    """[(start, end)] byte ranges of each rank's piece of one stream, from the
+    stream's block index (every block's byte offset, e.g. `block_index_dev`)
+    and the element `bounds` of `shard_bounds`."""
+    bs = block_size or default_block_size(elem_size)
+    offs = [int(v) for v in block_offsets]
+    starts = []
+    for s, e in bounds:
+        k = s // bs
+        starts.append(offs[k] if k < len(offs) and e > s else None)
+    out = []
+    nxt = stream_len
+    for r in range(len(bounds) - 1, -1, -1):
+        st = starts[r] if starts[r] is not None else nxt
+        out.append((st, nxt))
+        nxt = st
+    return out[::-1]
+
+
+def split_stream(buf, size, elem_size, world, block_size=0):
+    """Every rank's (element range, byte range) of the framed stream in device
+    tensor `buf` of `size` elements, from its block index: what a rank decodes
+    with `decompress_lz4_split(buf[b0:b1], ...)` when the compress side's piece
+    lengths are not at hand."""
+    from .api import block_index_dev
+    bounds = shard_bounds(size, elem_size, world, block_size)
+    offs = block_index_dev(buf, size, elem_size, block_size).cpu().tolist()
+    return list(zip(bounds, piece_ranges(offs, bounds, buf.numel(), elem_size, block_size)))

@@ -79,6 +79,17 @@ int64_t bshuf_decompress_lz4_dev_dlen(const void* in, const int64_t* d_in_nbytes
                                       void* ws, size_t ws_bytes, int64_t* d_result,
                                       const uint64_t* block_offsets, void* stream);
 
+/* The block index of a framed stream alone (the decoder's parallel header walk,
+ * replacing the reference's serial iochain walk, src/iochain.c:42-64): block k's
+ * byte offset into block_offsets[k] (device, bshuf_lz4_dev_nblocks() entries;
+ * ~0 for a block the walk could not place) and into *d_status 0 when the records
+ * tile the stream exactly, nonzero otherwise (decoding would return -91).  The
+ * workspace is bshuf_decompress_lz4_dev_workspace(in_nbytes, ...) bytes, or NULL
+ * (library pool).  For splitting one stream's decode across devices. */
+int64_t bshuf_lz4_block_index_dev(const void* in, size_t in_nbytes, size_t size, size_t elem_size,
+                                  size_t block_size, void* ws, size_t ws_bytes,
+                                  uint64_t* block_offsets, int64_t* d_status, void* stream);
+
 /* ---- batched device entry points (additive) ----
  *
  * `count` independent framed streams per call, all with the same elem_size and

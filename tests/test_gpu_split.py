@@ -13,6 +13,13 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
 SIZE = 3 * 1024 * 1024 + 4096 * 3 + 1005  # int16 elements: blocks split 2 ways + partial + tail
 
 
@@ -66,3 +73,27 @@ def test_split_stream_on_device_equals_single_stream():
     assert r0[4] == r0[5]  # joined pieces == the single stream
     assert r0[2] == len(r0[5]) and r0[3] == res[1][3] and res[1][1] == r0[3][0]
     assert r0[6] and res[1][6]
+
+
+def test_split_stream_from_block_index(torch):
+    """A whole device stream split by its block index (block_index_dev): the
+    index equals the encoder's own offsets, and every rank's byte range
+    decodes to its shard."""
+    import bitshuffle_amd as B
+    from bitshuffle_amd.api import block_index_dev
+    from bitshuffle_amd.split import decompress_lz4_split, split_stream
+    x = torch.empty(SIZE, dtype=torch.int16, device="cuda")
+    B.synth_fill_dev(x, 1)
+    nb = int(B.lib.bshuf_lz4_dev_nblocks(SIZE, 2, 0))
+    enc_offs = torch.empty(nb, dtype=torch.int64, device="cuda")
+    c = B.compress_lz4_dev(x, offsets=enc_offs)
+    assert torch.equal(block_index_dev(c, SIZE, 2), enc_offs)
+    for world in (2, 3, 5):
+        for (s, e), (b0, b1) in split_stream(c, SIZE, 2, world):
+            y = decompress_lz4_split(c[b0:b1], (e - s,), torch.int16)
+            assert torch.equal(y, x[s:e]), (world, s, e)
+    bad = c.clone()
+    bad[4096] ^= 0x55
+    bad[0:4] = 0  # first record length 0: the walk cannot tile the stream
+    with pytest.raises(B.BshufError):
+        block_index_dev(bad, SIZE, 2)

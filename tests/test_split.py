@@ -85,3 +85,25 @@ def test_split_stream_equals_single_stream(world, size, bs):
     assert [r[1] for r in res] == stream_offsets(lengths)[0]
     assert res[0][4] == want  # joined pieces == the single stream, byte for byte
     assert all(r[5] for r in res)  # every piece decodes to its shard
+
+
+def test_piece_ranges_from_block_index():
+    """Byte ranges from a block index equal the compress-side piece offsets
+    (oracle stream, its record headers walked on the host as the index)."""
+    from oracle import Oracle
+    from bitshuffle_amd.split import piece_ranges
+    o = Oracle()
+    size, bs = 9 * 4096 + 1005, 4096
+    x = o.gen_g1(size)
+    stream = o.compress_lz4(x, bs)
+    offs, p = [], 0
+    for _ in range(size // bs + (1 if size % bs >= 8 else 0)):
+        offs.append(p)
+        p += 4 + int.from_bytes(stream[p:p + 4].tobytes(), "big")
+    for world in (1, 2, 3, 4, 12):
+        bounds = shard_bounds(size, 2, world, bs)
+        pieces = [o.compress_lz4(x[s:e], bs).size if e > s else 0 for s, e in bounds]
+        want_offs, total = stream_offsets(pieces)
+        got = piece_ranges(offs, bounds, stream.size, 2, bs)
+        assert [g[0] for g in got] == want_offs and got[-1][1] == total == stream.size
+        assert [g[1] - g[0] for g in got] == pieces
