@@ -230,7 +230,8 @@ def decompress_lz4_dev(buf, shape, dtype, block_size=0, out=None, workspace=None
     want = buf.numel() if length is None else int(length.reshape(-1)[0].item())
     if count != want:
         raise BshufError("Decompressed different number of bytes than input buffer size."
-                         "Input buffer %d, decompressed %d." % (buf.numel(), count), count)
+                         "Input buffer %d, decompressed %d." % (want, count)
+                         + ("" if length is None else " (buffer capacity %d)" % buf.numel()), count)
     return out
 
 

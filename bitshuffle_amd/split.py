@@ -86,6 +86,18 @@ def compress_lz4_split(shard, block_size=0, elem_size=None, group=None, codec=No
     Returns (piece, offset, total, lengths): this rank's bytes of the single
     stream, where they start in it, its total length, and every rank's piece
     length.  Collective over `group` (every rank must call it)."""
+    import torch.distributed as dist
+    rank, world = ((dist.get_rank(group), dist.get_world_size(group))
+                   if dist.is_available() and dist.is_initialized() else (0, 1))
+    if rank != world - 1:
+        esz = elem_size if elem_size is not None else (
+            shard.element_size() if hasattr(shard, "element_size") else shard.dtype.itemsize)
+        nel = (shard.numel() * shard.element_size() // esz) if hasattr(shard, "numel") else shard.size
+        bs = block_size or default_block_size(esz)
+        if nel % bs:
+            raise ValueError("rank %d of %d holds %d elements, not a whole number of %d-element "
+                             "blocks: the joined pieces would not be one stream (use shard_bounds)"
+                             % (rank, world, nel, bs))
     if codec is None:
         import torch
         from .api import compress_lz4_dev
@@ -100,8 +112,6 @@ def compress_lz4_split(shard, block_size=0, elem_size=None, group=None, codec=No
         length, dev = len(piece), None
     lengths = _all_lengths(length, group, dev)
     offs, total = stream_offsets(lengths)
-    import torch.distributed as dist
-    rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
     return piece, offs[rank], total, lengths
 
 
@@ -125,8 +135,8 @@ def decompress_lz4_split(piece, shape, dtype, block_size=0, elem_size=None, code
 
 def gather_stream(piece, lengths, dst=0, group=None):
     """The whole stream on rank `dst` (a uint8 CPU tensor; None elsewhere):
-    every piece padded to the longest, one all-gather, trimmed and joined in
-    rank order."""
+    every piece padded to the longest, one gather to `dst` (only `dst` holds
+    world x the longest piece), trimmed and joined in rank order."""
     import torch
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized():
@@ -138,12 +148,12 @@ def gather_stream(piece, lengths, dst=0, group=None):
     buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
     mine = piece if isinstance(piece, torch.Tensor) else torch.as_tensor(piece)
     buf[: mine.numel()] = mine.to(dev).reshape(-1)
-    allb = torch.empty(world * mx, dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(allb, buf, group=group)
     if dist.get_rank(group) != dst:
+        dist.gather(buf, None, dst=dst, group=group)
         return None
-    allb = allb.cpu()
-    return torch.cat([allb[r * mx: r * mx + lengths[r]] for r in range(world)])
+    parts = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.gather(buf, parts, dst=dst, group=group)
+    return torch.cat([parts[r][: lengths[r]].cpu() for r in range(world)])
 
 
 def piece_ranges(block_offsets, bounds, stream_len, elem_size, block_size=0):
@@ -155,7 +165,15 @@ def piece_ranges(block_offsets, bounds, stream_len, elem_size, block_size=0):
     starts = []
     for s, e in bounds:
         k = s // bs
-        starts.append(offs[k] if k < len(offs) and e > s else None)
+        if e <= s:
+            starts.append(None)  # owns nothing: empty piece at the next start
+        elif k < len(offs):
+            starts.append(offs[k])
+        else:
+            # no record at all, only the raw `size % 8` tail (no partial block:
+            # size % bs < 8); the reference writes it after the last record
+            # (src/bitshuffle_core.c:1909-1926), so it is the stream's end.
+            starts.append(stream_len - (e - s) * elem_size)
     out = []
     nxt = stream_len
     for r in range(len(bounds) - 1, -1, -1):

@@ -673,16 +673,27 @@ def test_device_length_entry_points(bs, oracle, torch):
     big = torch.tensor([enc.size + 12345], dtype=torch.int64, device="cuda")
     y, r = bs.decompress_lz4_dev(buf, a.shape, torch.int16, sync=False, length=big)
     assert int(r.item()) == enc.size and y.cpu().numpy().tobytes() == a.tobytes()
-    # a corrupt stream: the host-length decoder's code
+    # a corrupt stream: the ORACLE's code for the same bytes (and the
+    # host-length device decoder's)
     bad = enc.copy()
     bad[4 + 40] ^= 0x5A  # inside block 0's payload
     bad[-30:] = 0        # and the tail end
+    with pytest.raises(RuntimeError) as orc:
+        oracle.decompress_lz4(bad, a.shape, np.int16)
     bbuf = torch.from_numpy(bad).cuda()
     with pytest.raises(RuntimeError) as single:
         bs.decompress_lz4_dev(bbuf, a.shape, torch.int16)
     ln = torch.tensor([bad.size], dtype=torch.int64, device="cuda")
     _, r = bs.decompress_lz4_dev(bbuf, a.shape, torch.int16, sync=False, length=ln)
-    assert int(r.item()) == single.value.args[1]
+    assert int(r.item()) == orc.value.args[1] == single.value.args[1]
+    # a payload-only corruption the decoder itself rejects (not the walk)
+    bad2 = enc.copy()
+    bad2[4:4 + 8] = 0xFF  # block 0: token 0xFF + 255-runs: literal length past the block
+    with pytest.raises(RuntimeError) as orc2:
+        oracle.decompress_lz4(bad2, a.shape, np.int16)
+    _, r = bs.decompress_lz4_dev(torch.from_numpy(bad2).cuda(), a.shape, torch.int16, sync=False,
+                                 length=torch.tensor([bad2.size], dtype=torch.int64, device="cuda"))
+    assert int(r.item()) == orc2.value.args[1]
     # batch: capacities from the bound, lengths from the compress results
     sizes = [3 * 4096 + 1005, 0, 17, 4096, 9 * 4096 + 13, 123457]
     arrs = [oracle.gen_g1(m, 1000 * i, 12345 + i) for i, m in enumerate(sizes)]

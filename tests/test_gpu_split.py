@@ -97,3 +97,24 @@ def test_split_stream_from_block_index(torch):
     bad[0:4] = 0  # first record length 0: the walk cannot tile the stream
     with pytest.raises(B.BshufError):
         block_index_dev(bad, SIZE, 2)
+
+
+@pytest.mark.parametrize("size,worlds", [(3 * 4096 + 5, (4, 5)), (2 * 4096 + 3, (3, 4)), (5, (2,))])
+def test_split_stream_tail_only_rank(torch, size, worlds):
+    """size % bs < 8 and more ranks than blocks: the last rank owns only the
+    raw tail (no record); its byte range is the stream's last (size % 8) * E
+    bytes (src/bitshuffle_core.c:1909-1926).  Stream checked against the oracle."""
+    import bitshuffle_amd as B
+    from oracle import Oracle
+    from bitshuffle_amd.split import decompress_lz4_split, split_stream
+    x = torch.empty(size, dtype=torch.int16, device="cuda")
+    B.synth_fill_dev(x, 1)
+    c = B.compress_lz4_dev(x)
+    assert c.cpu().numpy().tobytes() == Oracle().compress_lz4(x.cpu().numpy()).tobytes()
+    for world in worlds:
+        rng = split_stream(c, size, 2, world)
+        assert rng[-1][1] == (c.numel() - (size % 8) * 2, c.numel()) or size // 4096 >= world
+        assert rng[0][1][0] == 0 and all(rng[i][1][1] == rng[i + 1][1][0] for i in range(world - 1))
+        for (s, e), (b0, b1) in rng:
+            y = decompress_lz4_split(c[b0:b1], (e - s,), torch.int16)
+            assert torch.equal(y, x[s:e]), (world, s, e)

@@ -67,7 +67,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world,size,bs", [(2, 9 * 4096 + 1005, 4096), (3, 2 * 4096 + 13, 4096),
-                                           (3, 20 * 512 + 3, 512)])
+                                           (3, 20 * 512 + 3, 512), (4, 3 * 4096 + 5, 4096)])
 def test_split_stream_equals_single_stream(world, size, bs):
     from oracle import Oracle
     want = Oracle().compress_lz4(Oracle().gen_g1(size), bs).tobytes()
@@ -87,23 +87,54 @@ def test_split_stream_equals_single_stream(world, size, bs):
     assert all(r[5] for r in res)  # every piece decodes to its shard
 
 
-def test_piece_ranges_from_block_index():
+@pytest.mark.parametrize("size,worlds", [
+    (9 * 4096 + 1005, (1, 2, 3, 4, 12)),
+    # size % bs < 8: no partial block, the last rank owns only the raw tail
+    # whenever the world exceeds the block count
+    (3 * 4096 + 5, (1, 2, 3, 4, 5, 7)),
+    (2 * 4096 + 3, (2, 3, 4)),
+    (5, (1, 2, 3)),  # no block at all: the stream is the raw tail
+])
+def test_piece_ranges_from_block_index(size, worlds):
     """Byte ranges from a block index equal the compress-side piece offsets
     (oracle stream, its record headers walked on the host as the index)."""
     from oracle import Oracle
     from bitshuffle_amd.split import piece_ranges
     o = Oracle()
-    size, bs = 9 * 4096 + 1005, 4096
+    bs = 4096
     x = o.gen_g1(size)
     stream = o.compress_lz4(x, bs)
     offs, p = [], 0
     for _ in range(size // bs + (1 if size % bs >= 8 else 0)):
         offs.append(p)
         p += 4 + int.from_bytes(stream[p:p + 4].tobytes(), "big")
-    for world in (1, 2, 3, 4, 12):
+    for world in worlds:
         bounds = shard_bounds(size, 2, world, bs)
         pieces = [o.compress_lz4(x[s:e], bs).size if e > s else 0 for s, e in bounds]
         want_offs, total = stream_offsets(pieces)
         got = piece_ranges(offs, bounds, stream.size, 2, bs)
         assert [g[0] for g in got] == want_offs and got[-1][1] == total == stream.size
         assert [g[1] - g[0] for g in got] == pieces
+        # every piece decodes to its shard, and the pieces join to the stream
+        for (s, e), (b0, b1) in zip(bounds, got):
+            if e > s:
+                back = o.decompress_lz4(stream[b0:b1], (e - s,), np.int16, bs)
+                assert np.array_equal(back, x[s:e])
+
+
+def test_compress_split_rejects_ragged_shard():
+    """A rank other than the last must hold whole blocks; a torch.chunk-style
+    split would make pieces that do not join into one stream."""
+    import torch.distributed as dist
+    from bitshuffle_amd import split as sp
+    if dist.is_initialized():
+        pytest.skip("needs no default group")
+    orig = (dist.is_initialized, dist.get_rank, dist.get_world_size)
+    dist.is_initialized = lambda: True
+    dist.get_rank = lambda group=None: 0
+    dist.get_world_size = lambda group=None: 2
+    try:
+        with pytest.raises(ValueError, match="whole number"):
+            sp.compress_lz4_split(np.zeros(4096 + 8, np.int16), 4096, codec=_oracle_codec())
+    finally:
+        dist.is_initialized, dist.get_rank, dist.get_world_size = orig
