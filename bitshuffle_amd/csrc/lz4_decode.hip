@@ -404,6 +404,23 @@ __device__ __forceinline__ int small_mod(int x, int d, float rinv) {
     return r;
 }
 
+// Self-overlapping matches with a period dividing 4 and at most kDecPer bytes
+// run per lane in the batch's short-copy step (0: every self-overlapping
+// match by the wave; A/B builds with -DBSHUF_DEC_PER=N).
+#ifndef BSHUF_DEC_PER
+#define BSHUF_DEC_PER 16
+#endif
+// BSHUF_DEC_FILL1 (A/B builds only, off by default): wave fills of period 1 /
+// 2 / 4 from one read and masked dword writes (1: every dword masked, 2: only
+// the edge dwords) instead of the byte reads and byte edges below.  Bit-exact,
+// but measured slower (round 6, profiles/r06/dec_ab: k_lz4_decode 2 GiB G1
+// 0.779 -> 0.875 ms, G2 1.451 -> 1.782, E = 3 1.650 -> 1.951 with form 2).
+#ifndef BSHUF_DEC_FILL1
+#define BSHUF_DEC_FILL1 0
+#endif
+constexpr int kDecPer = BSHUF_DEC_PER;
+static_assert(kDecPer % 16 == 0 && kDecPer <= 64, "periodic per-lane fills: whole 16-byte pieces, <= 64");
+
 // The whole wave runs one match D[mop, mop+ml) = LZ4 copy from mop-off.
 // Non-overlapping (off >= ml): a plain forward copy.  Overlapping (off < ml):
 // the output is periodic with period off, byte i = D[mop-off + i mod off], so
@@ -421,6 +438,32 @@ __device__ __forceinline__ void wave_match(lds8* D, int mop, int off, int ml, in
         return;
     }
     const int s = mop - off;
+#if BSHUF_DEC_FILL1
+    if (off == 1 || off == 2 || off == 4) {
+        // a period dividing 4: ONE uniform read of the period's bytes, the
+        // pattern dword by v_perm (byte j = D[s + j mod off]), the same value
+        // rotated into every aligned dword of the fill, and one masked write
+        // per dword -- the edges included, so there are no byte writes and
+        // only the one LDS round trip
+        const uint32_t w = lds_rd32(D, s);
+        const uint32_t v = __builtin_amdgcn_perm(w, w, off == 1 ? 0x00000000u : off == 2 ? 0x01000100u
+                                                                                      : 0x03020100u);
+        const int a0 = mop & ~3, end = mop + ml;
+        // every aligned dword A holds pattern bytes from (A - s) mod off on
+        const uint32_t pv = __builtin_amdgcn_alignbit(v, v, 8u * ((uint32_t)(a0 - s) & 3u));
+        const int ndw = ((end + 3) >> 2) - (a0 >> 2);
+        const uint32_t base = (uint32_t)(uintptr_t)(D + a0);
+        for (int c = lane; c < ndw; c += kWave) {
+            const int A = a0 + 4 * c;
+            const uint32_t m = low_bytes_mask(end - A) & ~low_bytes_mask(mop - A);
+            if (BSHUF_DEC_FILL1 == 1 || m != 0xFFFFFFFFu)
+                lds_write_masked(base + 4u * (uint32_t)c, m, pv & m);
+            else
+                *(lds32*)(D + A) = pv;
+        }
+        return;
+    }
+#endif
     // v_rcp_f32 (1 ulp): small_mod's one correction step either way and the
     // [2^16/off, 2^16/off + 2) window below both absorb its error (x < 2^17)
     const float rinv = __builtin_amdgcn_rcpf((float)off);
@@ -649,7 +692,14 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
         const int mop = op + lit;
         const int rend = mop - off + min(ml, off);
         const uint64_t mm = (ABL & 2) ? 0ull : ballot(ml > 0);
-        const uint64_t cmask = mm & (ballot(ml > 16) | ballot(off < ml));  // only the head can overlap itself
+        // self-overlapping matches whose period divides 4 (offsets 1, 2, 4;
+        // offset 2 is 40 % of the matches of bit-shuffled int16 data) up to
+        // kDecPer bytes are periodic fills run by their own lane, 16 bytes
+        // per step from one pattern dword, beside the batch's short copies
+        const bool per = kDecPer > 0 && off < ml && ml <= kDecPer && (off == 1 || off == 2 || off == 4);
+        const uint64_t pm = ballot(per);
+        // the wave runs the long and the other self-overlapping matches
+        const uint64_t cmask = mm & (ballot(ml > 16) | ballot(off < ml)) & ~pm;
         uint64_t todo = mm;
         while (todo) {
             const int f = ffs64(todo);
@@ -657,7 +707,32 @@ __device__ __forceinline__ void lz4_exec_block(const Src& Cb, const int cp, lds8
             const uint64_t above = ~((2ull << f) - 1ull);  // lanes > f (none for f = 63)
             const uint64_t sm = ballot(rend > opf) & mm & above;
             const uint64_t batch = todo & (sm ? (1ull << ffs64(sm)) - 1ull : ~0ull);
-            if (__builtin_amdgcn_inverse_ballot_w64(batch & ~cmask)) lane_copy16(D, mop - off, D, mop, ml);
+            if constexpr (kDecPer > 0) {
+                if (__builtin_amdgcn_inverse_ballot_w64(batch & ~cmask)) {
+                    // one set of source reads serves both kinds: a copy's 16
+                    // bytes at mop - off, or a fill's period (its first bytes)
+                    const int sp = mop - off;
+                    const lds32* w = (const lds32*)(D + (sp & ~3));
+                    uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+                    uint32_t sh = (uint32_t)(sp & 3);
+                    if (per) {
+                        const uint32_t b = __builtin_amdgcn_alignbyte(x1, x0, sh);
+                        const uint32_t v = off == 4 ? b : off == 2 ? (b & 0xFFFFu) * 0x00010001u
+                                                                   : (b & 0xFFu) * 0x01010101u;
+                        x0 = x1 = x2 = x3 = x4 = v;
+                        sh = 0;
+                    }
+                    lane_put16(x0, x1, x2, x3, x4, sh, D, mop, min(ml, 16));
+#pragma unroll
+                    for (int k = 16; k < kDecPer; k += 16) {
+                        // 16 | the period: every later piece is the same pattern
+                        if (__builtin_amdgcn_inverse_ballot_w64(batch & pm & ballot(ml > k)))
+                            lane_put16(x0, x0, x0, x0, x0, 0u, D, mop + k, min(ml - k, 16));
+                    }
+                }
+            } else {
+                if (__builtin_amdgcn_inverse_ballot_w64(batch & ~cmask)) lane_copy16(D, mop - off, D, mop, ml);
+            }
             dg.count(1, 1);
             dg.count(2, (uint32_t)__builtin_popcountll(batch & cmask));
             for (uint64_t cm = batch & cmask; cm; cm &= cm - 1) {

@@ -2370,7 +2370,11 @@ hipError_t launch_big_t(const uint8_t* shuf, const Layout& L, const EncodeBufs& 
     const int64_t nb = L.nblocks();
     auto fn = k_lz4_encode_big<READBACK>;
     ProfScope prof("k_lz4_encode_big", s);
-    hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kWave), kTableBytes, s, shuf, L, b.scratch, b.slot, b.foot);
+#ifndef BSHUF_BIG_LDS_PAD
+#define BSHUF_BIG_LDS_PAD 0  // A/B builds only: fewer resident large blocks per CU
+#endif
+    hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(kWave), kTableBytes + BSHUF_BIG_LDS_PAD, s, shuf, L, b.scratch,
+                       b.slot, b.foot);
     return hipGetLastError();
 }
 

@@ -118,3 +118,42 @@ def test_split_stream_tail_only_rank(torch, size, worlds):
         for (s, e), (b0, b1) in rng:
             y = decompress_lz4_split(c[b0:b1], (e - s,), torch.int16)
             assert torch.equal(y, x[s:e]), (world, s, e)
+
+
+def _rccl_worker(port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        import bitshuffle_amd as B
+        from bitshuffle_amd.split import (compress_lz4_split, decompress_lz4_split, gather_stream,
+                                          shard_bounds)
+        size = 3 * 4096 + 5
+        x = torch.empty(size, dtype=torch.int16, device="cuda")
+        B.synth_fill_dev(x, 1)
+        s, e = shard_bounds(size, 2, 1)[0]
+        piece, off, total, lengths = compress_lz4_split(x[s:e].contiguous())
+        stream = gather_stream(piece, lengths)
+        back = decompress_lz4_split(piece, (e - s,), torch.int16)
+        q.put((dist.get_backend(), off, total, lengths, stream.numpy().tobytes(),
+               B.compress_lz4_dev(x).cpu().numpy().tobytes(), bool(torch.equal(back, x))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_collectives_on_rccl_world1():
+    """The RCCL ("nccl" backend) branch of split.py's collectives on device
+    tensors -- the all-gather of piece lengths and the gather to rank 0 -- at
+    world 1 (one GPU on this box; the gloo tests above cover worlds 2-5)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        backend, off, total, lengths, stream, whole, ok = q.get(timeout=150)
+    finally:
+        p.join(timeout=60)
+    assert backend == "nccl" and off == 0 and lengths == [len(whole)] and total == len(whole)
+    assert stream == whole and ok
