@@ -338,6 +338,9 @@ struct EmitBytes {
 // token / length / offset bytes around the run) take masked writes -- the
 // whole dwords between go out as plain writes, four per step, with no
 // per-piece mask arithmetic (lane_copy16 recomputes five masks per 16 bytes).
+#ifndef BSHUF_RUNS_PIPE
+#define BSHUF_RUNS_PIPE 1
+#endif
 __device__ __forceinline__ void lane_runs(const lds8* D, int sp, lds8* S, int dp, int n, bool mine) {
     const int k = dp & 3;
     const int b = sp - k;  // source byte of destination dword 0's byte 0 (may be < 0: masked off)
@@ -358,6 +361,42 @@ __device__ __forceinline__ void lane_runs(const lds8* D, int sp, lds8* S, int dp
         }
     }
     const int last = mine ? nd - 2 : 0;  // interior dwords 1 .. last
+#if BSHUF_RUNS_PIPE
+    // software-pipelined: the next step's four source dwords are read before
+    // this step's four writes (block and record are disjoint LDS), so a step
+    // waits for reads issued one step earlier instead of its own
+    if (ballot(1 <= last) == 0) return;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
+    if (1 <= last) {
+        a0 = W[1];
+        a1 = W[2];
+        a2 = W[3];
+        a3 = W[4];
+        a4 = W[5];
+    }
+    for (int t = 1;; t += 4) {
+        const bool more = t + 4 <= last;
+        uint32_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+        if (more) {
+            b1 = W[t + 5];
+            b2 = W[t + 6];
+            b3 = W[t + 7];
+            b4 = W[t + 8];
+        }
+        if (t <= last) {
+            O[t] = __builtin_amdgcn_alignbyte(a1, a0, r);
+            if (t + 1 <= last) O[t + 1] = __builtin_amdgcn_alignbyte(a2, a1, r);
+            if (t + 2 <= last) O[t + 2] = __builtin_amdgcn_alignbyte(a3, a2, r);
+            if (t + 3 <= last) O[t + 3] = __builtin_amdgcn_alignbyte(a4, a3, r);
+        }
+        if (ballot(more) == 0) break;
+        a0 = a4;
+        a1 = b1;
+        a2 = b2;
+        a3 = b3;
+        a4 = b4;
+    }
+#else
     for (int t = 1; ballot(t <= last) != 0; t += 4) {
         if (t <= last) {
             const uint32_t w0 = W[t], w1 = W[t + 1], w2 = W[t + 2], w3 = W[t + 3], w4 = W[t + 4];
@@ -367,6 +406,7 @@ __device__ __forceinline__ void lane_runs(const lds8* D, int sp, lds8* S, int dp
             if (t + 3 <= last) O[t + 3] = __builtin_amdgcn_alignbyte(w4, w3, r);
         }
     }
+#endif
 }
 
 // Builds the LZ4 bytes of a parsed block from its descriptors, wave-parallel
@@ -1842,6 +1882,9 @@ __device__ __forceinline__ void transpose4_regs_to_lds(const BlockRegs4<EK>& R, 
 // group k, three v_perm_b32), one 8x8 bit transpose per byte lane across those
 // eight registers (untranspose4_rows: the transpose is its own inverse) leaves
 // x[8b + j] = plane 8b + j of the four groups -- ONE dword per plane as above.
+#ifndef BSHUF_TR_SOFF
+#define BSHUF_TR_SOFF 1
+#endif
 template <int EK>
 __device__ __forceinline__ void transpose4s_regs_to_lds(const BlockRegs4<EK>& R, lds8* D, int P,
                                                         int lane) {
@@ -1864,8 +1907,20 @@ __device__ __forceinline__ void transpose4s_regs_to_lds(const BlockRegs4<EK>& R,
                 }
             }
             untranspose4_rows<EK>(x);
+            // plane r's dword of this lane at Dq + r * rs: the row offsets are
+            // wave-uniform (scalar multiplies), not per-lane 64-bit mads
+            lds8* const Dq = D + 4 * q;
+            const int rs = 4 * P4;
+            int ro = 0;
 #pragma unroll
-            for (int r = 0; r < 8 * EK; r++) D32[r * P4 + q] = x[r];
+            for (int r = 0; r < 8 * EK; r++) {
+                *(lds32*)(Dq + ro) = x[r];
+                ro += rs;
+                // E >= 4: an opaque scalar (one v_add per row instead of a
+                // 64-bit v_mad per row; 1 GiB G2 -2.2 %, E = 2 measured flat or
+                // worse beside the pipelined lane_runs, profiles/r06/enc_ab)
+                if constexpr (BSHUF_TR_SOFF && EK >= 4) asm volatile("" : "+s"(ro));
+            }
         }
     }
 }
