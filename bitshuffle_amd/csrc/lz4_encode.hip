@@ -1953,6 +1953,9 @@ __device__ __forceinline__ void raw_to_lds(const RawRegs& R, lds8* S, int nbytes
     }
 }
 
+#ifndef BSHUF_FLUSH4
+#define BSHUF_FLUSH4 1  // A/B builds: 0 = round 5's copy-out and zeroing loops
+#endif
 // Persistent: workgroup w handles blocks w, w+G, w+2G, ...  While block k is
 // parsed out of LDS, the 8 KiB of block k+G are already in flight into
 // registers, so HBM latency hides under the (LDS-latency-bound) parse.
@@ -2011,13 +2014,34 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
     // Deferred copy-out (A/B variant 4096 turns it off): a block's record
     // stays in the table's LDS until the next block is transposed.
     constexpr bool kDefer = (EK != 0 || BSHUF_EK0_DEFER) && (VAR & 4096) == 0;
+    constexpr bool kFlush4 = BSHUF_FLUSH4 && EK != 4;
     int64_t pend_blk = -1;
     int pend_c = 0;
     auto flush_pending = [&]() {
         if (pend_blk < 0) return;
         uint8_t* po = a.scratch + pend_blk * a.slot;
         const int nch = (4 + pend_c + 15) >> 4;
-        for (int i = lane; i < nch; i += kWave) ((gbl128*)po)[i] = ((const lds128*)L0)[i];
+        // up to four 16-byte chunks per lane read before any is stored: one
+        // LDS round trip per 4 KiB of record instead of one per KiB (with the
+        // unrolled table zeroing below: 1 GiB G1 0.299 -> 0.297 ms, E = 3
+        // 1.055 -> 1.040; E = 4 0.788 -> 0.809, so not there; each change
+        // alone measured worse, profiles/r06/enc_ab)
+        if constexpr (kFlush4) {
+        for (int i0 = 0; i0 < nch; i0 += 4 * kWave) {
+            // (reads past the record stay inside the table's 16 KiB: a staged
+            // record has nch <= 1024 chunks, so i0 <= 768 and i < 1024)
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = ((const lds128*)L0)[i0 + u * kWave + lane];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * kWave + lane;
+                if (i < nch) ((gbl128*)po)[i] = v[u];
+            }
+        }
+        } else {
+            for (int i = lane; i < nch; i += kWave) ((gbl128*)po)[i] = ((const lds128*)L0)[i];
+        }
         if (lane == 0) a.foot[pend_blk] = 4 + (uint64_t)pend_c;
         pend_blk = -1;
     };
@@ -2116,8 +2140,14 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
             // next iteration's wait for that prefetch finds them long done
             // (issued at the end of a parse, they would hold it up instead)
             flush_pending();
-            for (int i = lane; i < kTableBytes / 16; i += kWave)
-                ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
+            if constexpr (kFlush4) {
+#pragma unroll
+                for (int k = 0; k < kTableBytes / 16 / kWave; k++)
+                    ((lds128*)L0)[k * kWave + lane] = u32x4{0u, 0u, 0u, 0u};
+            } else {
+                for (int i = lane; i < kTableBytes / 16; i += kWave)
+                    ((lds128*)L0)[i] = u32x4{0u, 0u, 0u, 0u};
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
