@@ -246,7 +246,9 @@ constexpr int kLaneRunMin = 4;             // ... when the batch has at least th
 constexpr int kDescMax = 256;              // descriptor slots per block
 constexpr int kDescBytes = 8 * kDescMax;   // LDS behind the block
 
-// Sequence s's descriptor: two dwords in LDS (ip | off << 16, lit | mc << 16),
+// Sequence s's descriptor: two dwords in LDS (ip | off << 16, lit | ml << 16,
+// ml = mc + kMinMatch: the match length itself, which the asm re-test loop has
+// at hand without the subtraction),
 // stored by every lane (same address, same value: no exec-mask switch on the
 // parse's chain).  The record size is not tracked during the parse:
 // emit_sequences' prefix sum gives it.
@@ -260,7 +262,7 @@ struct EmitDesc {
     // block with the inline emitter when ns ends above kDescMax.
     __device__ __forceinline__ bool seq(int& op, int anchor, int ip, int off, int mc) {
         ((lds64v*)desc)[min(ns, kDescMax - 1)] = u32x2{(uint32_t)ip | ((uint32_t)off << 16),
-                                                      (uint32_t)(ip - anchor) | ((uint32_t)mc << 16)};
+                                                      (uint32_t)(ip - anchor) | ((uint32_t)(mc + kMinMatch) << 16)};
         ns++;
         (void)op;
         return true;
@@ -430,7 +432,7 @@ __device__ __forceinline__ int emit_sequences(const lds8* D, const Em& em, const
             ip = (int)(x & 0xFFFFu);
             off = (int)(x >> 16);
             lit = (int)(y & 0xFFFFu);
-            mc = (int)(y >> 16);
+            mc = (int)(y >> 16) - kMinMatch;
         }
         const int le = lz4_ext_bytes(lit), me = m ? lz4_ext_bytes(mc) : 0;
         const int len = act ? 1 + le + lit + (m ? 2 + me : 0) : 0;
@@ -608,7 +610,7 @@ struct EmitDescV {
         const int slot = ns & (kWave - 1);
         if (lane == slot) {
             dlo = (uint32_t)ip | ((uint32_t)off << 16);
-            dhi = (uint32_t)(ip - anchor) | ((uint32_t)mc << 16);
+            dhi = (uint32_t)(ip - anchor) | ((uint32_t)(mc + kMinMatch) << 16);
         }
         ns++;
         if ((ns & (kWave - 1)) == 0) store_batch(ns - kWave, kWave);
@@ -727,7 +729,8 @@ enum { kRtLimit = 0, kRtMiss = 1, kRtSlow = 2, kRtLong = 3 };
         /* ---- sequence descriptor -> lane ns % 64 of dlo / dhi */ \
         "s_sub_u32 %[t0], %[ip], %[ref]\n\t" \
         "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t" \
-        "s_pack_ll_b32_b16 %[t1], %[lit], %[mc]\n\t" \
+        "s_add_u32 %[t1], %[mc], 4\n\t" \
+        "s_pack_ll_b32_b16 %[t1], %[lit], %[t1]\n\t" \
         "s_and_b32 m0, %[ns], 63\n\t" \
         "s_add_u32 %[ns], %[ns], 1\n\t" \
         "s_add_u32 %[ip], %[ip], %[mc]\n\t" \
@@ -998,8 +1001,12 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
     uint32_t vn, vy, vz, vd0, vc2, vcb, val, vah, vbl, vbh;
     asm volatile(
         "s_mov_b32 %[keep], m0\n\t"
+        /* m0 = the descriptor lane (ns % 64), ns = the batch base (ns - m0);
+           ns = base + m0 again at the exit */
+        "s_and_b32 m0, %[ns], 63\n\t"
+        "s_andn2_b32 %[ns], %[ns], 63\n\t"
         "s_cmp_eq_u32 %[entry], 1\n\t"
-        "s_cbranch_scc1 L_top%=\n\t"
+        "s_cbranch_scc1 L_cent%=\n\t"
         /* ======== a search from p0 = ip: the first window's bytes */
         "L_nsrch%=:\n\t"
         "v_add_u32 %[vh], %[ip], %[lanev]\n\t"
@@ -1115,36 +1122,42 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
         "s_cmpk_eq_u32 %[t3], 0x100\n\t"
         "s_cbranch_scc1 L_eslow%=\n\t"
         "s_sub_u32 %[ip], %[mpos], %[t4]\n\t"
-        "s_sub_u32 %[ref], %[mref], %[t4]\n\t"
+        "s_sub_u32 %[c2], %[mref], %[t4]\n\t"
         "s_add_u32 %[mc], %[t3], %[t4]\n\t"
-        "s_sub_u32 %[mc], %[mc], 4\n\t"
         "s_sub_u32 %[lit], %[ip], %[anchor]\n\t"
         "s_mov_b32 %[tb], %[mpos]\n\t"
-        /* ======== the re-test chain (retest_chain) */
-        "L_top%=:\n\t"
-        "s_sub_u32 %[t0], %[ip], %[ref]\n\t"
+        /* ======== the re-test chain (retest_chain).  Round 6: in here mc
+           holds the match length ml = mc + 4 (the descriptor's field), the
+           candidate stays in c2, and a loop iteration has no literals and
+           starts from the previous count window based at the previous ip,
+           so ip - tb = ml: no ref / tb / lit bookkeeping per sequence.
+           L_tope: a sequence with literals, count window based at tb (the
+           search's hand-off above falls into it; L_cent, the entry from C++
+           with mc beyond kMinMatch and the candidate in ref, jumps to it);
+           the loop's own head is the tail of the count below. */
+        "L_tope%=:\n\t"
+        "s_sub_u32 %[t0], %[ip], %[c2]\n\t"
         "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t"
         "s_pack_ll_b32_b16 %[t1], %[lit], %[mc]\n\t"
-        "s_and_b32 m0, %[ns], 63\n\t"
-        "s_add_u32 %[ns], %[ns], 1\n\t"
         "s_add_u32 %[ip], %[ip], %[mc]\n\t"
+        "s_sub_u32 %[mc], %[ip], %[tb]\n\t"
+        /* descriptor -> lane ns % 64 of dlo / dhi; mc = ip - tb from here */
+        "L_desc%=:\n\t"
         "v_writelane_b32 %[dlo], %[t0], m0\n\t"
         "v_writelane_b32 %[dhi], %[t1], m0\n\t"
-        "s_and_b32 %[t2], %[ns], 63\n\t"
-        "s_cbranch_scc0 L_flush%=\n\t"
+        "s_add_u32 m0, m0, 1\n\t"
+        "s_cmp_eq_u32 m0, 64\n\t"
+        "s_cbranch_scc1 L_flush%=\n\t"
         "L_flushed%=:\n\t"
-        "s_add_u32 %[ip], %[ip], 4\n\t"
-        "s_mov_b32 %[lit], 0\n\t"
         "s_cmp_ge_i32 %[ip], %[limit]\n\t"
         "s_cbranch_scc1 L_lim%=\n\t"
-        "s_sub_u32 %[t0], %[ip], %[tb]\n\t"
-        "s_sub_u32 %[t1], %[t0], 2\n\t"
+        "s_sub_u32 %[t1], %[mc], 2\n\t"
         "s_cmp_gt_u32 %[t1], 249\n\t"
         "s_cbranch_scc1 L_slow%=\n\t"
         "v_mov_b32_dpp %[vn], %[tail] wave_shl:1 bound_ctrl:0\n\t"
-        "s_and_b32 %[t2], %[t0], 3\n\t"
+        "s_and_b32 %[t2], %[mc], 3\n\t"
         "s_and_b32 %[t3], %[t1], 3\n\t"
-        "s_lshr_b32 %[t0], %[t0], 2\n\t"
+        "s_lshr_b32 %[t0], %[mc], 2\n\t"
         "v_alignbyte_b32 %[vy], %[vn], %[tail], %[t2]\n\t"
         "v_alignbyte_b32 %[vz], %[vn], %[tail], %[t3]\n\t"
         "s_lshr_b32 %[t1], %[t1], 2\n\t"
@@ -1171,7 +1184,6 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
         "ds_read_u16 %[vc2], %[vz]\n\t"
         "ds_write_b16 %[vz], %[vd0]\n\t"
         "s_and_b32 %[t3], %[ip], 3\n\t"
-        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t"
         "s_waitcnt lgkmcnt(1)\n\t"
         "v_and_b32 %[vcb], -4, %[vc2]\n\t"
         "v_add_u32 %[vcb], %[vcb], %[lane4d]\n\t"
@@ -1189,26 +1201,33 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
         "s_cbranch_scc1 L_miss%=\n\t"
         "s_cmp_eq_u64 vcc, 0\n\t"
         "s_cbranch_scc1 L_long%=\n\t"
+        /* count: ml = the first differing byte of the window from ip (its
+           first 4 bytes are the tested ones), capped at mlimit - ip */
         "s_ff1_i32_b64 %[t0], vcc\n\t"
-        "s_mov_b32 %[ref], %[c2]\n\t"
+        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t"
         "v_readlane_b32 %[t2], %[vbh], %[t0]\n\t"
         "s_lshl_b32 %[t0], %[t0], 2\n\t"
-        "s_mov_b32 %[tb], %[ip]\n\t"
         "s_ff1_i32_b32 %[t2], %[t2]\n\t"
         "s_lshr_b32 %[t2], %[t2], 3\n\t"
         "s_add_u32 %[t0], %[t0], %[t2]\n\t"
-        "s_min_i32 %[t0], %[t0], %[t1]\n\t"
-        "s_sub_u32 %[mc], %[t0], 4\n\t"
-        "s_branch L_top%=\n\t"
+        "s_min_i32 %[mc], %[t0], %[t1]\n\t"
+        /* the next sequence's descriptor fields (no literals) and ip */
+        "s_sub_u32 %[t0], %[ip], %[c2]\n\t"
+        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t"
+        "s_lshl_b32 %[t1], %[mc], 16\n\t"
+        "s_add_u32 %[ip], %[ip], %[mc]\n\t"
+        "s_branch L_desc%=\n\t"
         /* a batch of 64 descriptors to LDS (dropped past kDescMax) */
         "L_flush%=:\n\t"
-        "s_sub_u32 %[t2], %[ns], 64\n\t"
-        "s_cmp_ge_u32 %[t2], 256\n\t"
-        "s_cbranch_scc1 L_flushed%=\n\t"
-        "s_lshl_b32 %[t2], %[t2], 3\n\t"
+        "s_mov_b32 m0, 0\n\t"
+        "s_cmp_ge_u32 %[ns], 256\n\t" /* kDescMax */
+        "s_cbranch_scc1 L_fldone%=\n\t"
+        "s_lshl_b32 %[t2], %[ns], 3\n\t"
         "s_add_u32 %[t2], %[t2], %[desc]\n\t"
         "v_add_u32 %[vcb], %[t2], %[lane8]\n\t"
         "ds_write2_b32 %[vcb], %[dlo], %[dhi] offset1:1\n\t"
+        "L_fldone%=:\n\t"
+        "s_add_u32 %[ns], %[ns], 64\n\t"
         "s_branch L_flushed%=\n\t"
         /* offset-2 shortcut (retest_chain) */
         "L_p2%=:\n\t"
@@ -1230,7 +1249,6 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
         "v_mov_b32_dpp %[vbh], %[tail] wave_shr:1 bound_ctrl:0\n\t"
         "v_alignbyte_b32 %[vbl], %[tail], %[vbh], 2\n\t"
         "v_writelane_b32 %[vbl], %[t1], 0\n\t"
-        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t"
         "s_branch L_cmp%=\n\t"
         /* ======== a re-test miss: search from anchor + 1 */
         "L_miss%=:\n\t"
@@ -1252,9 +1270,14 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
         "s_mov_b32 %[code], 3\n\t"
         "s_mov_b32 %[anchor], %[ip]\n\t"
         "s_branch L_end%=\n\t"
+        "L_cent%=:\n\t"
+        "s_add_u32 %[mc], %[mc], 4\n\t"
+        "s_mov_b32 %[c2], %[ref]\n\t"
+        "s_branch L_tope%=\n\t"
         "L_eslow%=:\n\t"
         "s_mov_b32 %[code], 4\n\t"
         "L_end%=:\n\t"
+        "s_add_u32 %[ns], %[ns], m0\n\t"
         "s_mov_b32 m0, %[keep]"
         : [code] "=&s"(code), [ip] "+s"(ip), [anchor] "+s"(anchor), [ref] "+s"(ref), [mc] "+s"(mc),
           [lit] "+s"(lit), [ns] "+s"(ns), [tb] "+s"(tb), [nwin] "+s"(nwin), [mpos] "+s"(mpos),
