@@ -987,7 +987,343 @@ __device__ __forceinline__ void search_entry(const int mpos, const int mref, con
 //               catch-up reaches 64 bytes back or whose count reaches 256.
 // Wait states as in the three blocks it is made of.
 enum { kPcLimit = 0, kPcPartial = 1, kPcSlow = 2, kPcLong = 3, kPcEntry = 4 };
+// lz4_encode_block OPT bit (not a bshuf_set_variant value): parse_chain's
+// count-first compare (the element size decides, see BSHUF_CMP_COUNT_FIRST)
+constexpr int kOptCountFirst = 1 << 23;
 
+// The re-test's compare of the 4 bytes at ip and the count window, in two
+// forms (round 6, profiles/r06/enc_ab r6r/r6s): miss-first tests lane 0 by
+// itself (2 instructions) before the count's per-lane work, so a re-test miss
+// costs what it did; count-first computes the per-lane count beside the one
+// unsigned compare that tells miss and "all equal" apart, 2 instructions fewer
+// per hit and 7 more per miss.  1 GiB per launch, miss-first / count-first
+// against the form before: G2 0.766 -> 0.759 / 0.747, E = 3 1.027 -> 1.019 /
+// 1.032, E = 12 0.986 -> 0.977 / 0.984, G1 0.294 -> 0.294 / 0.293: G2 float32
+// (142 hits, 25 misses per block) takes count-first, every other element size
+// miss-first.
+#define BSHUF_PARSE_ASM(CMP_BLOCK, RARE_BLOCK) \
+    asm volatile( \
+        "s_mov_b32 %[keep], m0\n\t" \
+        /* m0 = the descriptor lane (ns % 64), ns = the batch base (ns - m0); \
+           ns = base + m0 again at the exit */ \
+        "s_and_b32 m0, %[ns], 63\n\t" \
+        "s_andn2_b32 %[ns], %[ns], 63\n\t" \
+        "s_cmp_eq_u32 %[entry], 1\n\t" \
+        "s_cbranch_scc1 L_cent%=\n\t" \
+        /* ======== a search from p0 = ip: the first window's bytes */ \
+        "L_nsrch%=:\n\t" \
+        "v_add_u32 %[vh], %[ip], %[lanev]\n\t" \
+        "v_min_i32 %[vh], %[n], %[vh]\n\t" \
+        "v_and_b32 %[va], -4, %[vh]\n\t" \
+        "ds_read_b32 %[vlo], %[va] offset:16384\n\t" \
+        "ds_read_b32 %[vhi], %[va] offset:16388\n\t" \
+        "v_and_b32 %[vh], 3, %[vh]\n\t" \
+        "v_add_u32 %[vpos], %[ip], %[pq_off]\n\t" \
+        "v_add_u32 %[vnxt], %[ip], %[pq_nxt]\n\t" \
+        "v_mov_b32 %[vstep], %[pq_stp]\n\t" \
+        "s_add_u32 %[qs], %[ip], 64\n\t" \
+        "s_movk_i32 %[qstep], 0x7f\n\t" \
+        "s_mov_b32 %[nwin], 0\n\t" \
+        "s_waitcnt lgkmcnt(0)\n\t" \
+        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[vh]\n\t" \
+        /* ======== full search windows (search_chain) */ \
+        "L_stop%=:\n\t" \
+        "s_cmp_gt_i32 %[qs], %[limit]\n\t" \
+        "s_cbranch_scc1 L_spart%=\n\t" \
+        "v_mul_lo_u32 %[vh], %[vseq], %[kmul]\n\t" \
+        "v_min_i32 %[va], %[n], %[vnxt]\n\t" \
+        "s_add_u32 %[qs], %[qs], %[qstep]\n\t" \
+        "s_add_u32 %[qstep], %[qstep], 64\n\t" \
+        "v_lshrrev_b32 %[vsh], 15, %[vh]\n\t" \
+        "v_lshrrev_b32 %[vad], 18, %[vh]\n\t" \
+        "v_and_b32 %[vsh], 16, %[vsh]\n\t" \
+        "v_and_b32 %[vad], 0x3ffc, %[vad]\n\t" \
+        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t" \
+        "v_lshlrev_b32 %[vd], %[vsh], %[vpos]\n\t" \
+        "v_and_b32 %[vh], -4, %[va]\n\t" \
+        "ds_mskor_rtn_b32 %[vold], %[vad], %[vm], %[vd]\n\t" \
+        "ds_read_b32 %[vlo], %[vh] offset:16384\n\t" \
+        "ds_read_b32 %[vhi], %[vh] offset:16388\n\t" \
+        "v_and_b32 %[va], 3, %[va]\n\t" \
+        "s_waitcnt lgkmcnt(2)\n\t" \
+        "v_lshrrev_b32 %[vcand], %[vsh], %[vold]\n\t" \
+        "v_bfe_u32 %[vm], %[vold], %[vsh], 2\n\t" \
+        "v_and_b32 %[vd], 0xfffc, %[vcand]\n\t" \
+        "ds_read_b32 %[vold], %[vd] offset:16384\n\t" \
+        "ds_read_b32 %[vx1], %[vd] offset:16388\n\t" \
+        "s_waitcnt lgkmcnt(0)\n\t" \
+        "v_alignbyte_b32 %[vold], %[vx1], %[vold], %[vm]\n\t" \
+        "v_cmp_eq_u32 vcc, %[vold], %[vseq]\n\t" \
+        "s_cbranch_vccnz L_smatch%=\n\t" \
+        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[va]\n\t" \
+        "v_mov_b32 %[vpos], %[vnxt]\n\t" \
+        "v_add_u32 %[vnxt], %[vnxt], %[vstep]\n\t" \
+        "v_add_u32 %[vstep], 64, %[vstep]\n\t" \
+        "s_add_u32 %[nwin], %[nwin], 1\n\t" \
+        "s_branch L_stop%=\n\t" \
+        /* ======== a match at lane js: later lanes whose found entry is \
+           <= mpos put it back (positions after the match were never inserted) */ \
+        "L_smatch%=:\n\t" \
+        "s_ff1_i32_b64 %[t0], vcc\n\t" \
+        "v_and_b32 %[vd], 0xffff, %[vcand]\n\t" \
+        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t" \
+        "v_lshlrev_b32 %[vx1], %[vsh], %[vd]\n\t" \
+        "v_readlane_b32 %[mpos], %[vpos], %[t0]\n\t" \
+        "v_readlane_b32 %[mref], %[vd], %[t0]\n\t" \
+        "s_lshl_b64 %[sy], -2, %[t0]\n\t" \
+        "v_cmp_ge_u32 %[sz], %[mpos], %[vd]\n\t" \
+        "s_and_b64 %[sy], %[sy], %[sz]\n\t" \
+        "s_and_saveexec_b64 %[sz], %[sy]\n\t" \
+        "ds_mskor_b32 %[vad], %[vm], %[vx1]\n\t" \
+        "s_mov_b64 exec, %[sz]\n\t" \
+        /* ======== catch-up (64 bytes back) and the first count window from \
+           mpos, one LDS round trip (search_entry) */ \
+        "s_and_b32 %[t0], %[mpos], -4\n\t" \
+        "s_and_b32 %[t1], %[mref], -4\n\t" \
+        "v_add_u32 %[vx1], %[t0], %[lane4d]\n\t" \
+        "v_add_u32 %[vbh], %[t1], %[lane4d]\n\t" \
+        "s_add_u32 %[t2], %[mpos], -1\n\t" \
+        "s_add_u32 %[t3], %[mref], -1\n\t" \
+        "ds_read_b32 %[val], %[vx1]\n\t" \
+        "ds_read_b32 %[vah], %[vx1] offset:4\n\t" \
+        "ds_read_b32 %[vbl], %[vbh]\n\t" \
+        "ds_read_b32 %[vbh], %[vbh] offset:4\n\t" \
+        "v_sub_u32 %[vy], %[t2], %[lanev]\n\t" \
+        "v_sub_u32 %[vz], %[t3], %[lanev]\n\t" \
+        "v_max_i32 %[vn], 0, %[vy]\n\t" \
+        "v_max_i32 %[vd0], 0, %[vz]\n\t" \
+        "ds_read_u8 %[vn], %[vn] offset:16384\n\t" \
+        "ds_read_u8 %[vd0], %[vd0] offset:16384\n\t" \
+        "s_and_b32 %[t0], %[mpos], 3\n\t" \
+        "s_and_b32 %[t1], %[mref], 3\n\t" \
+        "s_sub_u32 %[t2], %[mlimit], %[mpos]\n\t" \
+        "s_max_i32 %[t2], %[t2], 0\n\t" \
+        "s_waitcnt lgkmcnt(2)\n\t" \
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t0]\n\t" \
+        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t1]\n\t" \
+        "v_xor_b32 %[vx1], %[tail], %[vbl]\n\t" \
+        "v_cmp_ne_u32 %[ne], %[tail], %[vbl]\n\t" \
+        "v_cmp_le_i32 %[sy], %[anchor], %[vy]\n\t" \
+        "v_cmp_le_i32 %[sz], 0, %[vz]\n\t" \
+        "s_ff1_i32_b64 %[t3], %[ne]\n\t" \
+        "s_waitcnt lgkmcnt(0)\n\t" \
+        "v_readlane_b32 %[t4], %[vx1], %[t3]\n\t" \
+        "v_cmp_eq_u32 %[bm], %[vn], %[vd0]\n\t" \
+        "s_lshl_b32 %[t3], %[t3], 2\n\t" \
+        "s_ff1_i32_b32 %[t4], %[t4]\n\t" \
+        "s_lshr_b32 %[t4], %[t4], 3\n\t" \
+        "s_add_u32 %[t3], %[t3], %[t4]\n\t" \
+        "s_cmp_eq_u64 %[ne], 0\n\t" \
+        "s_cselect_b32 %[t3], 256, %[t3]\n\t" \
+        "s_min_i32 %[t3], %[t3], %[t2]\n\t" \
+        "s_and_b64 %[bm], %[bm], %[sy]\n\t" \
+        "s_and_b64 %[bm], %[bm], %[sz]\n\t" \
+        "s_not_b64 %[bm], %[bm]\n\t" \
+        "s_ff1_i32_b64 %[t4], %[bm]\n\t" \
+        "s_cmp_lt_i32 %[t4], 0\n\t" \
+        "s_cbranch_scc1 L_eslow%=\n\t" \
+        "s_cmpk_eq_u32 %[t3], 0x100\n\t" \
+        "s_cbranch_scc1 L_eslow%=\n\t" \
+        "s_sub_u32 %[ip], %[mpos], %[t4]\n\t" \
+        "s_sub_u32 %[c2], %[mref], %[t4]\n\t" \
+        "s_add_u32 %[mc], %[t3], %[t4]\n\t" \
+        "s_sub_u32 %[lit], %[ip], %[anchor]\n\t" \
+        "s_mov_b32 %[tb], %[mpos]\n\t" \
+        /* ======== the re-test chain (retest_chain).  Round 6: in here mc \
+           holds the match length ml = mc + 4 (the descriptor's field), the \
+           candidate stays in c2, and a loop iteration has no literals and \
+           starts from the previous count window based at the previous ip, \
+           so ip - tb = ml: no ref / tb / lit bookkeeping per sequence. \
+           L_tope: a sequence with literals, count window based at tb (the \
+           search's hand-off above falls into it; L_cent, the entry from C++ \
+           with mc beyond kMinMatch and the candidate in ref, jumps to it); \
+           the loop's own head is the tail of the count below. */ \
+        "L_tope%=:\n\t" \
+        "s_sub_u32 %[t0], %[ip], %[c2]\n\t" \
+        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t" \
+        "s_pack_ll_b32_b16 %[t1], %[lit], %[mc]\n\t" \
+        "s_add_u32 %[ip], %[ip], %[mc]\n\t" \
+        "s_sub_u32 %[mc], %[ip], %[tb]\n\t" \
+        /* descriptor -> lane ns % 64 of dlo / dhi; mc = ip - tb from here */ \
+        "L_desc%=:\n\t" \
+        "v_writelane_b32 %[dlo], %[t0], m0\n\t" \
+        "v_writelane_b32 %[dhi], %[t1], m0\n\t" \
+        "s_add_u32 m0, m0, 1\n\t" \
+        "s_cmp_eq_u32 m0, 64\n\t" \
+        "s_cbranch_scc1 L_flush%=\n\t" \
+        "L_flushed%=:\n\t" \
+        "s_cmp_ge_i32 %[ip], %[limit]\n\t" \
+        "s_cbranch_scc1 L_lim%=\n\t" \
+        "s_sub_u32 %[t1], %[mc], 2\n\t" \
+        "s_cmp_gt_u32 %[t1], 249\n\t" \
+        "s_cbranch_scc1 L_slow%=\n\t" \
+        "v_mov_b32_dpp %[vn], %[tail] wave_shl:1 bound_ctrl:0\n\t" \
+        "s_and_b32 %[t2], %[mc], 3\n\t" \
+        "s_and_b32 %[t3], %[t1], 3\n\t" \
+        "s_lshr_b32 %[t0], %[mc], 2\n\t" \
+        "v_alignbyte_b32 %[vy], %[vn], %[tail], %[t2]\n\t" \
+        "v_alignbyte_b32 %[vz], %[vn], %[tail], %[t3]\n\t" \
+        "s_lshr_b32 %[t1], %[t1], 2\n\t" \
+        "s_sub_u32 %[t2], %[ip], 2\n\t" \
+        "v_readlane_b32 %[t0], %[vy], %[t0]\n\t" \
+        "v_readlane_b32 %[t1], %[vz], %[t1]\n\t" \
+        "s_cmp_eq_u32 %[t0], %[t1]\n\t" \
+        "s_cbranch_scc1 L_p2%=\n\t" \
+        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t" \
+        "s_mul_i32 %[t1], %[t1], 0x9e3779b1\n\t" \
+        "s_lshr_b32 %[t0], %[t0], 18\n\t" \
+        "s_lshr_b32 %[t1], %[t1], 18\n\t" \
+        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t" \
+        "s_and_b32 %[t1], %[t1], 0x3ffe\n\t" \
+        "s_and_b32 %[t3], %[ip], -4\n\t" \
+        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t" \
+        "v_mov_b32 %[vn], %[t1]\n\t" \
+        "v_mov_b32 %[vy], %[t2]\n\t" \
+        "v_mov_b32 %[vz], %[t0]\n\t" \
+        "v_mov_b32 %[vd0], %[ip]\n\t" \
+        "ds_read_b32 %[val], %[vcb]\n\t" \
+        "ds_read_b32 %[vah], %[vcb] offset:4\n\t" \
+        "ds_write_b16 %[vn], %[vy]\n\t" \
+        "ds_read_u16 %[vc2], %[vz]\n\t" \
+        "ds_write_b16 %[vz], %[vd0]\n\t" \
+        "s_and_b32 %[t3], %[ip], 3\n\t" \
+        "s_waitcnt lgkmcnt(1)\n\t" \
+        "v_and_b32 %[vcb], -4, %[vc2]\n\t" \
+        "v_add_u32 %[vcb], %[vcb], %[lane4d]\n\t" \
+        "ds_read_b32 %[vbl], %[vcb]\n\t" \
+        "ds_read_b32 %[vbh], %[vcb] offset:4\n\t" \
+        "v_readfirstlane_b32 %[c2], %[vc2]\n\t" \
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t" \
+        "s_and_b32 %[t2], %[c2], 3\n\t" \
+        "s_waitcnt lgkmcnt(0)\n\t" \
+        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t2]\n\t" \
+        CMP_BLOCK \
+        /* count: ml = the first differing byte of the window from ip (its \
+           first 4 bytes are the tested ones), capped at mlimit - ip */ \
+        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t" \
+        "v_readlane_b32 %[t2], %[vbh], %[t0]\n\t" \
+        "s_min_i32 %[mc], %[t2], %[t1]\n\t" \
+        /* the next sequence's descriptor fields (no literals) and ip */ \
+        "s_sub_u32 %[t0], %[ip], %[c2]\n\t" \
+        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t" \
+        "s_lshl_b32 %[t1], %[mc], 16\n\t" \
+        "s_add_u32 %[ip], %[ip], %[mc]\n\t" \
+        "s_branch L_desc%=\n\t" \
+        /* a batch of 64 descriptors to LDS (dropped past kDescMax) */ \
+        "L_flush%=:\n\t" \
+        "s_mov_b32 m0, 0\n\t" \
+        "s_cmp_ge_u32 %[ns], 256\n\t" /* kDescMax */ \
+        "s_cbranch_scc1 L_fldone%=\n\t" \
+        "s_lshl_b32 %[t2], %[ns], 3\n\t" \
+        "s_add_u32 %[t2], %[t2], %[desc]\n\t" \
+        "v_add_u32 %[vcb], %[t2], %[lane8]\n\t" \
+        "ds_write2_b32 %[vcb], %[dlo], %[dhi] offset1:1\n\t" \
+        "L_fldone%=:\n\t" \
+        "s_add_u32 %[ns], %[ns], 64\n\t" \
+        "s_branch L_flushed%=\n\t" \
+        /* offset-2 shortcut (retest_chain) */ \
+        "L_p2%=:\n\t" \
+        "s_and_b32 %[t3], %[ip], -4\n\t" \
+        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t" \
+        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t" \
+        "ds_read_b32 %[val], %[vcb]\n\t" \
+        "ds_read_b32 %[vah], %[vcb] offset:4\n\t" \
+        "s_lshr_b32 %[t0], %[t0], 18\n\t" \
+        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t" \
+        "v_mov_b32 %[vd0], %[ip]\n\t" \
+        "v_mov_b32 %[vz], %[t0]\n\t" \
+        "ds_write_b16 %[vz], %[vd0]\n\t" \
+        "s_and_b32 %[t3], %[ip], 3\n\t" \
+        "s_sub_u32 %[c2], %[ip], 2\n\t" \
+        "s_waitcnt lgkmcnt(1)\n\t" \
+        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t" \
+        "s_nop 1\n\t" \
+        "v_mov_b32_dpp %[vbh], %[tail] wave_shr:1 bound_ctrl:0\n\t" \
+        "v_alignbyte_b32 %[vbl], %[tail], %[vbh], 2\n\t" \
+        "v_writelane_b32 %[vbl], %[t1], 0\n\t" \
+        "s_branch L_cmp%=\n\t" \
+        /* ======== a re-test miss: search from anchor + 1 */ \
+        RARE_BLOCK \
+        "L_miss%=:\n\t" \
+        "s_mov_b32 %[anchor], %[ip]\n\t" \
+        "s_add_u32 %[ip], %[ip], 1\n\t" \
+        "s_branch L_nsrch%=\n\t" \
+        "L_lim%=:\n\t" \
+        "s_mov_b32 %[code], 0\n\t" \
+        "s_mov_b32 %[anchor], %[ip]\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_spart%=:\n\t" \
+        "s_mov_b32 %[code], 1\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_slow%=:\n\t" \
+        "s_mov_b32 %[code], 2\n\t" \
+        "s_mov_b32 %[anchor], %[ip]\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_long%=:\n\t" \
+        "s_mov_b32 %[code], 3\n\t" \
+        "s_mov_b32 %[anchor], %[ip]\n\t" \
+        "s_branch L_end%=\n\t" \
+        "L_cent%=:\n\t" \
+        "s_add_u32 %[mc], %[mc], 4\n\t" \
+        "s_mov_b32 %[c2], %[ref]\n\t" \
+        "s_branch L_tope%=\n\t" \
+        "L_eslow%=:\n\t" \
+        "s_mov_b32 %[code], 4\n\t" \
+        "L_end%=:\n\t" \
+        "s_add_u32 %[ns], %[ns], m0\n\t" \
+        "s_mov_b32 m0, %[keep]" \
+        : [code] "=&s"(code), [ip] "+s"(ip), [anchor] "+s"(anchor), [ref] "+s"(ref), [mc] "+s"(mc), \
+          [lit] "+s"(lit), [ns] "+s"(ns), [tb] "+s"(tb), [nwin] "+s"(nwin), [mpos] "+s"(mpos), \
+          [mref] "+s"(mref), [c2] "+s"(c2), [t0] "=&s"(t0), [t1] "=&s"(t1), [t2] "=&s"(t2), \
+          [t3] "=&s"(t3), [t4] "=&s"(t4), [keep] "=&s"(keep), [qs] "=&s"(qs), [qstep] "=&s"(qstep), \
+          [ne] "=&s"(ne), [bm] "=&s"(bm), [sy] "=&s"(sy), [sz] "=&s"(sz), [tail] "+v"(tail), \
+          [dlo] "+v"(dlo), [dhi] "+v"(dhi), [vseq] "+v"(vseq), [vpos] "+v"(vpos), [vh] "=&v"(vh), \
+          [va] "=&v"(va), [vsh] "=&v"(vsh), [vad] "=&v"(vad), [vm] "=&v"(vm), [vd] "=&v"(vd), \
+          [vold] "=&v"(vold), [vlo] "=&v"(vlo), [vhi] "=&v"(vhi), [vx1] "=&v"(vx1), [vnxt] "=&v"(vnxt), \
+          [vstep] "=&v"(vstep), [vcand] "=&v"(vcand), [vn] "=&v"(vn), [vy] "=&v"(vy), [vz] "=&v"(vz), \
+          [vd0] "=&v"(vd0), [vc2] "=&v"(vc2), [vcb] "=&v"(vcb), [val] "=&v"(val), [vah] "=&v"(vah), \
+          [vbl] "=&v"(vbl), [vbh] "=&v"(vbh) \
+        : [entry] "s"(entry), [limit] "s"(limit), [mlimit] "s"(mlimit), [n] "s"(n), [desc] "s"(desc), \
+          [kmul] "s"(2654435761u), [ffff] "s"(0xFFFFu), [lane4d] "v"(lane4d), [lane8] "v"(lane8), \
+          [lanev] "v"(lanev), [pq_off] "v"(pq_off), [pq_nxt] "v"(pq_nxt), [pq_stp] "v"(pq_stp) \
+        : "vcc", "scc", "memory")
+
+#define BSHUF_CMP_MISS_FIRST \
+        "L_cmp%=:\n\t" \
+        "v_cmp_ne_u32 vcc, %[tail], %[vbl]\n\t" \
+        "v_xor_b32 %[vbh], %[tail], %[vbl]\n\t" \
+        "s_bitcmp1_b32 vcc_lo, 0\n\t" \
+        "s_cbranch_scc1 L_miss%=\n\t" \
+        /* every lane: the window byte of its first difference (4 lane + \
+           first differing bit / 8; garbage in equal lanes, never read), \
+           beside the scalar tests */ \
+        "v_ffbl_b32 %[vbh], %[vbh]\n\t" \
+        "v_lshrrev_b32 %[vbh], 3, %[vbh]\n\t" \
+        "v_lshl_add_u32 %[vbh], %[lanev], 2, %[vbh]\n\t" \
+        "s_ff1_i32_b64 %[t0], vcc\n\t" \
+        "s_cmp_lt_i32 %[t0], 0\n\t" \
+        "s_cbranch_scc1 L_long%=\n\t"
+#define BSHUF_CMP_COUNT_FIRST \
+        "L_cmp%=:\n\t" \
+        /* every lane: the window byte of its first difference (4 lane + \
+           first differing bit / 8; garbage in equal lanes, never read) */ \
+        "v_cmp_ne_u32 vcc, %[tail], %[vbl]\n\t" \
+        "v_xor_b32 %[vbh], %[tail], %[vbl]\n\t" \
+        "v_ffbl_b32 %[vbh], %[vbh]\n\t" \
+        "v_lshrrev_b32 %[vbh], 3, %[vbh]\n\t" \
+        "v_lshl_add_u32 %[vbh], %[lanev], 2, %[vbh]\n\t" \
+        /* the first differing lane: 0 = the 4-byte test failed (miss), none \
+           = all 256 bytes equal (long), both by one unsigned compare */ \
+        "s_ff1_i32_b64 %[t0], vcc\n\t" \
+        "s_sub_u32 %[t3], %[t0], 1\n\t" \
+        "s_cmp_gt_u32 %[t3], 62\n\t" \
+        "s_cbranch_scc1 L_rare%=\n\t"
+#define BSHUF_RARE_COUNT_FIRST \
+        "L_rare%=:\n\t" \
+        "s_cmp_lg_u32 %[t0], 0\n\t" \
+        "s_cbranch_scc1 L_long%=\n\t"
+
+template <bool kMissFirst>
 __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor, int& ref, int& mc, int& lit,
                                            int& ns, int& tb, int& nwin, int& mpos, int& mref, int& c2,
                                            uint32_t& tail, uint32_t& dlo, uint32_t& dhi, uint32_t& vseq,
@@ -999,301 +1335,10 @@ __device__ __forceinline__ int parse_chain(const int entry, int& ip, int& anchor
     uint64_t ne, bm, sy, sz;
     uint32_t vh, va, vsh, vad, vm, vd, vold, vlo, vhi, vx1, vnxt, vstep, vcand;
     uint32_t vn, vy, vz, vd0, vc2, vcb, val, vah, vbl, vbh;
-    asm volatile(
-        "s_mov_b32 %[keep], m0\n\t"
-        /* m0 = the descriptor lane (ns % 64), ns = the batch base (ns - m0);
-           ns = base + m0 again at the exit */
-        "s_and_b32 m0, %[ns], 63\n\t"
-        "s_andn2_b32 %[ns], %[ns], 63\n\t"
-        "s_cmp_eq_u32 %[entry], 1\n\t"
-        "s_cbranch_scc1 L_cent%=\n\t"
-        /* ======== a search from p0 = ip: the first window's bytes */
-        "L_nsrch%=:\n\t"
-        "v_add_u32 %[vh], %[ip], %[lanev]\n\t"
-        "v_min_i32 %[vh], %[n], %[vh]\n\t"
-        "v_and_b32 %[va], -4, %[vh]\n\t"
-        "ds_read_b32 %[vlo], %[va] offset:16384\n\t"
-        "ds_read_b32 %[vhi], %[va] offset:16388\n\t"
-        "v_and_b32 %[vh], 3, %[vh]\n\t"
-        "v_add_u32 %[vpos], %[ip], %[pq_off]\n\t"
-        "v_add_u32 %[vnxt], %[ip], %[pq_nxt]\n\t"
-        "v_mov_b32 %[vstep], %[pq_stp]\n\t"
-        "s_add_u32 %[qs], %[ip], 64\n\t"
-        "s_movk_i32 %[qstep], 0x7f\n\t"
-        "s_mov_b32 %[nwin], 0\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[vh]\n\t"
-        /* ======== full search windows (search_chain) */
-        "L_stop%=:\n\t"
-        "s_cmp_gt_i32 %[qs], %[limit]\n\t"
-        "s_cbranch_scc1 L_spart%=\n\t"
-        "v_mul_lo_u32 %[vh], %[vseq], %[kmul]\n\t"
-        "v_min_i32 %[va], %[n], %[vnxt]\n\t"
-        "s_add_u32 %[qs], %[qs], %[qstep]\n\t"
-        "s_add_u32 %[qstep], %[qstep], 64\n\t"
-        "v_lshrrev_b32 %[vsh], 15, %[vh]\n\t"
-        "v_lshrrev_b32 %[vad], 18, %[vh]\n\t"
-        "v_and_b32 %[vsh], 16, %[vsh]\n\t"
-        "v_and_b32 %[vad], 0x3ffc, %[vad]\n\t"
-        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t"
-        "v_lshlrev_b32 %[vd], %[vsh], %[vpos]\n\t"
-        "v_and_b32 %[vh], -4, %[va]\n\t"
-        "ds_mskor_rtn_b32 %[vold], %[vad], %[vm], %[vd]\n\t"
-        "ds_read_b32 %[vlo], %[vh] offset:16384\n\t"
-        "ds_read_b32 %[vhi], %[vh] offset:16388\n\t"
-        "v_and_b32 %[va], 3, %[va]\n\t"
-        "s_waitcnt lgkmcnt(2)\n\t"
-        "v_lshrrev_b32 %[vcand], %[vsh], %[vold]\n\t"
-        "v_bfe_u32 %[vm], %[vold], %[vsh], 2\n\t"
-        "v_and_b32 %[vd], 0xfffc, %[vcand]\n\t"
-        "ds_read_b32 %[vold], %[vd] offset:16384\n\t"
-        "ds_read_b32 %[vx1], %[vd] offset:16388\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_alignbyte_b32 %[vold], %[vx1], %[vold], %[vm]\n\t"
-        "v_cmp_eq_u32 vcc, %[vold], %[vseq]\n\t"
-        "s_cbranch_vccnz L_smatch%=\n\t"
-        "v_alignbyte_b32 %[vseq], %[vhi], %[vlo], %[va]\n\t"
-        "v_mov_b32 %[vpos], %[vnxt]\n\t"
-        "v_add_u32 %[vnxt], %[vnxt], %[vstep]\n\t"
-        "v_add_u32 %[vstep], 64, %[vstep]\n\t"
-        "s_add_u32 %[nwin], %[nwin], 1\n\t"
-        "s_branch L_stop%=\n\t"
-        /* ======== a match at lane js: later lanes whose found entry is
-           <= mpos put it back (positions after the match were never inserted) */
-        "L_smatch%=:\n\t"
-        "s_ff1_i32_b64 %[t0], vcc\n\t"
-        "v_and_b32 %[vd], 0xffff, %[vcand]\n\t"
-        "v_lshlrev_b32 %[vm], %[vsh], %[ffff]\n\t"
-        "v_lshlrev_b32 %[vx1], %[vsh], %[vd]\n\t"
-        "v_readlane_b32 %[mpos], %[vpos], %[t0]\n\t"
-        "v_readlane_b32 %[mref], %[vd], %[t0]\n\t"
-        "s_lshl_b64 %[sy], -2, %[t0]\n\t"
-        "v_cmp_ge_u32 %[sz], %[mpos], %[vd]\n\t"
-        "s_and_b64 %[sy], %[sy], %[sz]\n\t"
-        "s_and_saveexec_b64 %[sz], %[sy]\n\t"
-        "ds_mskor_b32 %[vad], %[vm], %[vx1]\n\t"
-        "s_mov_b64 exec, %[sz]\n\t"
-        /* ======== catch-up (64 bytes back) and the first count window from
-           mpos, one LDS round trip (search_entry) */
-        "s_and_b32 %[t0], %[mpos], -4\n\t"
-        "s_and_b32 %[t1], %[mref], -4\n\t"
-        "v_add_u32 %[vx1], %[t0], %[lane4d]\n\t"
-        "v_add_u32 %[vbh], %[t1], %[lane4d]\n\t"
-        "s_add_u32 %[t2], %[mpos], -1\n\t"
-        "s_add_u32 %[t3], %[mref], -1\n\t"
-        "ds_read_b32 %[val], %[vx1]\n\t"
-        "ds_read_b32 %[vah], %[vx1] offset:4\n\t"
-        "ds_read_b32 %[vbl], %[vbh]\n\t"
-        "ds_read_b32 %[vbh], %[vbh] offset:4\n\t"
-        "v_sub_u32 %[vy], %[t2], %[lanev]\n\t"
-        "v_sub_u32 %[vz], %[t3], %[lanev]\n\t"
-        "v_max_i32 %[vn], 0, %[vy]\n\t"
-        "v_max_i32 %[vd0], 0, %[vz]\n\t"
-        "ds_read_u8 %[vn], %[vn] offset:16384\n\t"
-        "ds_read_u8 %[vd0], %[vd0] offset:16384\n\t"
-        "s_and_b32 %[t0], %[mpos], 3\n\t"
-        "s_and_b32 %[t1], %[mref], 3\n\t"
-        "s_sub_u32 %[t2], %[mlimit], %[mpos]\n\t"
-        "s_max_i32 %[t2], %[t2], 0\n\t"
-        "s_waitcnt lgkmcnt(2)\n\t"
-        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t0]\n\t"
-        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t1]\n\t"
-        "v_xor_b32 %[vx1], %[tail], %[vbl]\n\t"
-        "v_cmp_ne_u32 %[ne], %[tail], %[vbl]\n\t"
-        "v_cmp_le_i32 %[sy], %[anchor], %[vy]\n\t"
-        "v_cmp_le_i32 %[sz], 0, %[vz]\n\t"
-        "s_ff1_i32_b64 %[t3], %[ne]\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_readlane_b32 %[t4], %[vx1], %[t3]\n\t"
-        "v_cmp_eq_u32 %[bm], %[vn], %[vd0]\n\t"
-        "s_lshl_b32 %[t3], %[t3], 2\n\t"
-        "s_ff1_i32_b32 %[t4], %[t4]\n\t"
-        "s_lshr_b32 %[t4], %[t4], 3\n\t"
-        "s_add_u32 %[t3], %[t3], %[t4]\n\t"
-        "s_cmp_eq_u64 %[ne], 0\n\t"
-        "s_cselect_b32 %[t3], 256, %[t3]\n\t"
-        "s_min_i32 %[t3], %[t3], %[t2]\n\t"
-        "s_and_b64 %[bm], %[bm], %[sy]\n\t"
-        "s_and_b64 %[bm], %[bm], %[sz]\n\t"
-        "s_not_b64 %[bm], %[bm]\n\t"
-        "s_ff1_i32_b64 %[t4], %[bm]\n\t"
-        "s_cmp_lt_i32 %[t4], 0\n\t"
-        "s_cbranch_scc1 L_eslow%=\n\t"
-        "s_cmpk_eq_u32 %[t3], 0x100\n\t"
-        "s_cbranch_scc1 L_eslow%=\n\t"
-        "s_sub_u32 %[ip], %[mpos], %[t4]\n\t"
-        "s_sub_u32 %[c2], %[mref], %[t4]\n\t"
-        "s_add_u32 %[mc], %[t3], %[t4]\n\t"
-        "s_sub_u32 %[lit], %[ip], %[anchor]\n\t"
-        "s_mov_b32 %[tb], %[mpos]\n\t"
-        /* ======== the re-test chain (retest_chain).  Round 6: in here mc
-           holds the match length ml = mc + 4 (the descriptor's field), the
-           candidate stays in c2, and a loop iteration has no literals and
-           starts from the previous count window based at the previous ip,
-           so ip - tb = ml: no ref / tb / lit bookkeeping per sequence.
-           L_tope: a sequence with literals, count window based at tb (the
-           search's hand-off above falls into it; L_cent, the entry from C++
-           with mc beyond kMinMatch and the candidate in ref, jumps to it);
-           the loop's own head is the tail of the count below. */
-        "L_tope%=:\n\t"
-        "s_sub_u32 %[t0], %[ip], %[c2]\n\t"
-        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t"
-        "s_pack_ll_b32_b16 %[t1], %[lit], %[mc]\n\t"
-        "s_add_u32 %[ip], %[ip], %[mc]\n\t"
-        "s_sub_u32 %[mc], %[ip], %[tb]\n\t"
-        /* descriptor -> lane ns % 64 of dlo / dhi; mc = ip - tb from here */
-        "L_desc%=:\n\t"
-        "v_writelane_b32 %[dlo], %[t0], m0\n\t"
-        "v_writelane_b32 %[dhi], %[t1], m0\n\t"
-        "s_add_u32 m0, m0, 1\n\t"
-        "s_cmp_eq_u32 m0, 64\n\t"
-        "s_cbranch_scc1 L_flush%=\n\t"
-        "L_flushed%=:\n\t"
-        "s_cmp_ge_i32 %[ip], %[limit]\n\t"
-        "s_cbranch_scc1 L_lim%=\n\t"
-        "s_sub_u32 %[t1], %[mc], 2\n\t"
-        "s_cmp_gt_u32 %[t1], 249\n\t"
-        "s_cbranch_scc1 L_slow%=\n\t"
-        "v_mov_b32_dpp %[vn], %[tail] wave_shl:1 bound_ctrl:0\n\t"
-        "s_and_b32 %[t2], %[mc], 3\n\t"
-        "s_and_b32 %[t3], %[t1], 3\n\t"
-        "s_lshr_b32 %[t0], %[mc], 2\n\t"
-        "v_alignbyte_b32 %[vy], %[vn], %[tail], %[t2]\n\t"
-        "v_alignbyte_b32 %[vz], %[vn], %[tail], %[t3]\n\t"
-        "s_lshr_b32 %[t1], %[t1], 2\n\t"
-        "s_sub_u32 %[t2], %[ip], 2\n\t"
-        "v_readlane_b32 %[t0], %[vy], %[t0]\n\t"
-        "v_readlane_b32 %[t1], %[vz], %[t1]\n\t"
-        "s_cmp_eq_u32 %[t0], %[t1]\n\t"
-        "s_cbranch_scc1 L_p2%=\n\t"
-        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t"
-        "s_mul_i32 %[t1], %[t1], 0x9e3779b1\n\t"
-        "s_lshr_b32 %[t0], %[t0], 18\n\t"
-        "s_lshr_b32 %[t1], %[t1], 18\n\t"
-        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t"
-        "s_and_b32 %[t1], %[t1], 0x3ffe\n\t"
-        "s_and_b32 %[t3], %[ip], -4\n\t"
-        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t"
-        "v_mov_b32 %[vn], %[t1]\n\t"
-        "v_mov_b32 %[vy], %[t2]\n\t"
-        "v_mov_b32 %[vz], %[t0]\n\t"
-        "v_mov_b32 %[vd0], %[ip]\n\t"
-        "ds_read_b32 %[val], %[vcb]\n\t"
-        "ds_read_b32 %[vah], %[vcb] offset:4\n\t"
-        "ds_write_b16 %[vn], %[vy]\n\t"
-        "ds_read_u16 %[vc2], %[vz]\n\t"
-        "ds_write_b16 %[vz], %[vd0]\n\t"
-        "s_and_b32 %[t3], %[ip], 3\n\t"
-        "s_waitcnt lgkmcnt(1)\n\t"
-        "v_and_b32 %[vcb], -4, %[vc2]\n\t"
-        "v_add_u32 %[vcb], %[vcb], %[lane4d]\n\t"
-        "ds_read_b32 %[vbl], %[vcb]\n\t"
-        "ds_read_b32 %[vbh], %[vcb] offset:4\n\t"
-        "v_readfirstlane_b32 %[c2], %[vc2]\n\t"
-        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t"
-        "s_and_b32 %[t2], %[c2], 3\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_alignbyte_b32 %[vbl], %[vbh], %[vbl], %[t2]\n\t"
-        "L_cmp%=:\n\t"
-        "v_cmp_ne_u32 vcc, %[tail], %[vbl]\n\t"
-        "v_xor_b32 %[vbh], %[tail], %[vbl]\n\t"
-        "s_bitcmp1_b32 vcc_lo, 0\n\t"
-        "s_cbranch_scc1 L_miss%=\n\t"
-        "s_cmp_eq_u64 vcc, 0\n\t"
-        "s_cbranch_scc1 L_long%=\n\t"
-        /* count: ml = the first differing byte of the window from ip (its
-           first 4 bytes are the tested ones), capped at mlimit - ip */
-        "s_ff1_i32_b64 %[t0], vcc\n\t"
-        "s_sub_u32 %[t1], %[mlimit], %[ip]\n\t"
-        "v_readlane_b32 %[t2], %[vbh], %[t0]\n\t"
-        "s_lshl_b32 %[t0], %[t0], 2\n\t"
-        "s_ff1_i32_b32 %[t2], %[t2]\n\t"
-        "s_lshr_b32 %[t2], %[t2], 3\n\t"
-        "s_add_u32 %[t0], %[t0], %[t2]\n\t"
-        "s_min_i32 %[mc], %[t0], %[t1]\n\t"
-        /* the next sequence's descriptor fields (no literals) and ip */
-        "s_sub_u32 %[t0], %[ip], %[c2]\n\t"
-        "s_pack_ll_b32_b16 %[t0], %[ip], %[t0]\n\t"
-        "s_lshl_b32 %[t1], %[mc], 16\n\t"
-        "s_add_u32 %[ip], %[ip], %[mc]\n\t"
-        "s_branch L_desc%=\n\t"
-        /* a batch of 64 descriptors to LDS (dropped past kDescMax) */
-        "L_flush%=:\n\t"
-        "s_mov_b32 m0, 0\n\t"
-        "s_cmp_ge_u32 %[ns], 256\n\t" /* kDescMax */
-        "s_cbranch_scc1 L_fldone%=\n\t"
-        "s_lshl_b32 %[t2], %[ns], 3\n\t"
-        "s_add_u32 %[t2], %[t2], %[desc]\n\t"
-        "v_add_u32 %[vcb], %[t2], %[lane8]\n\t"
-        "ds_write2_b32 %[vcb], %[dlo], %[dhi] offset1:1\n\t"
-        "L_fldone%=:\n\t"
-        "s_add_u32 %[ns], %[ns], 64\n\t"
-        "s_branch L_flushed%=\n\t"
-        /* offset-2 shortcut (retest_chain) */
-        "L_p2%=:\n\t"
-        "s_and_b32 %[t3], %[ip], -4\n\t"
-        "v_add_u32 %[vcb], %[t3], %[lane4d]\n\t"
-        "s_mul_i32 %[t0], %[t0], 0x9e3779b1\n\t"
-        "ds_read_b32 %[val], %[vcb]\n\t"
-        "ds_read_b32 %[vah], %[vcb] offset:4\n\t"
-        "s_lshr_b32 %[t0], %[t0], 18\n\t"
-        "s_and_b32 %[t0], %[t0], 0x3ffe\n\t"
-        "v_mov_b32 %[vd0], %[ip]\n\t"
-        "v_mov_b32 %[vz], %[t0]\n\t"
-        "ds_write_b16 %[vz], %[vd0]\n\t"
-        "s_and_b32 %[t3], %[ip], 3\n\t"
-        "s_sub_u32 %[c2], %[ip], 2\n\t"
-        "s_waitcnt lgkmcnt(1)\n\t"
-        "v_alignbyte_b32 %[tail], %[vah], %[val], %[t3]\n\t"
-        "s_nop 1\n\t"
-        "v_mov_b32_dpp %[vbh], %[tail] wave_shr:1 bound_ctrl:0\n\t"
-        "v_alignbyte_b32 %[vbl], %[tail], %[vbh], 2\n\t"
-        "v_writelane_b32 %[vbl], %[t1], 0\n\t"
-        "s_branch L_cmp%=\n\t"
-        /* ======== a re-test miss: search from anchor + 1 */
-        "L_miss%=:\n\t"
-        "s_mov_b32 %[anchor], %[ip]\n\t"
-        "s_add_u32 %[ip], %[ip], 1\n\t"
-        "s_branch L_nsrch%=\n\t"
-        "L_lim%=:\n\t"
-        "s_mov_b32 %[code], 0\n\t"
-        "s_mov_b32 %[anchor], %[ip]\n\t"
-        "s_branch L_end%=\n\t"
-        "L_spart%=:\n\t"
-        "s_mov_b32 %[code], 1\n\t"
-        "s_branch L_end%=\n\t"
-        "L_slow%=:\n\t"
-        "s_mov_b32 %[code], 2\n\t"
-        "s_mov_b32 %[anchor], %[ip]\n\t"
-        "s_branch L_end%=\n\t"
-        "L_long%=:\n\t"
-        "s_mov_b32 %[code], 3\n\t"
-        "s_mov_b32 %[anchor], %[ip]\n\t"
-        "s_branch L_end%=\n\t"
-        "L_cent%=:\n\t"
-        "s_add_u32 %[mc], %[mc], 4\n\t"
-        "s_mov_b32 %[c2], %[ref]\n\t"
-        "s_branch L_tope%=\n\t"
-        "L_eslow%=:\n\t"
-        "s_mov_b32 %[code], 4\n\t"
-        "L_end%=:\n\t"
-        "s_add_u32 %[ns], %[ns], m0\n\t"
-        "s_mov_b32 m0, %[keep]"
-        : [code] "=&s"(code), [ip] "+s"(ip), [anchor] "+s"(anchor), [ref] "+s"(ref), [mc] "+s"(mc),
-          [lit] "+s"(lit), [ns] "+s"(ns), [tb] "+s"(tb), [nwin] "+s"(nwin), [mpos] "+s"(mpos),
-          [mref] "+s"(mref), [c2] "+s"(c2), [t0] "=&s"(t0), [t1] "=&s"(t1), [t2] "=&s"(t2),
-          [t3] "=&s"(t3), [t4] "=&s"(t4), [keep] "=&s"(keep), [qs] "=&s"(qs), [qstep] "=&s"(qstep),
-          [ne] "=&s"(ne), [bm] "=&s"(bm), [sy] "=&s"(sy), [sz] "=&s"(sz), [tail] "+v"(tail),
-          [dlo] "+v"(dlo), [dhi] "+v"(dhi), [vseq] "+v"(vseq), [vpos] "+v"(vpos), [vh] "=&v"(vh),
-          [va] "=&v"(va), [vsh] "=&v"(vsh), [vad] "=&v"(vad), [vm] "=&v"(vm), [vd] "=&v"(vd),
-          [vold] "=&v"(vold), [vlo] "=&v"(vlo), [vhi] "=&v"(vhi), [vx1] "=&v"(vx1), [vnxt] "=&v"(vnxt),
-          [vstep] "=&v"(vstep), [vcand] "=&v"(vcand), [vn] "=&v"(vn), [vy] "=&v"(vy), [vz] "=&v"(vz),
-          [vd0] "=&v"(vd0), [vc2] "=&v"(vc2), [vcb] "=&v"(vcb), [val] "=&v"(val), [vah] "=&v"(vah),
-          [vbl] "=&v"(vbl), [vbh] "=&v"(vbh)
-        : [entry] "s"(entry), [limit] "s"(limit), [mlimit] "s"(mlimit), [n] "s"(n), [desc] "s"(desc),
-          [kmul] "s"(2654435761u), [ffff] "s"(0xFFFFu), [lane4d] "v"(lane4d), [lane8] "v"(lane8),
-          [lanev] "v"(lanev), [pq_off] "v"(pq_off), [pq_nxt] "v"(pq_nxt), [pq_stp] "v"(pq_stp)
-        : "vcc", "scc", "memory");
+    if constexpr (kMissFirst)
+        BSHUF_PARSE_ASM(BSHUF_CMP_MISS_FIRST, );
+    else
+        BSHUF_PARSE_ASM(BSHUF_CMP_COUNT_FIRST, BSHUF_RARE_COUNT_FIRST);
     return code;
 }
 
@@ -1336,7 +1381,7 @@ __device__ int lz4_encode_block(const Blk D, const int n, const Table<WIDE> T, E
                 entry = uni(entry), ip = uni(ip), anchor = uni(anchor), ref = uni(ref), mc = uni(mc);
                 lit = uni(lit), em.ns = uni(em.ns), tb = uni(tb), nwin = uni(nwin), mpos = uni(mpos);
                 mref = uni(mref), c2 = uni(c2);
-                const int code = parse_chain(entry, ip, anchor, ref, mc, lit, em.ns, tb, nwin, mpos, mref, c2,
+                const int code = parse_chain<(OPT & kOptCountFirst) == 0>(entry, ip, anchor, ref, mc, lit, em.ns, tb, nwin, mpos, mref, c2,
                                              tail, em.dlo, em.dhi, vseq, vpos, limit, mlimit, n, desc_addr,
                                              lane4d, lane8, (uint32_t)lane, pq_off, pq_nxt, pq_stp);
                 if (code == kPcLimit) break;
@@ -2204,7 +2249,8 @@ __global__ __launch_bounds__(64) void k_lz4_encode(EncArgs a, int64_t nb) {
                 // descriptors are buffered in VGPRs
                 using Em = typename std::conditional<(VAR & 8192) != 0, EmitDescV, EmitDesc>::type;
                 Em em{(lds32*)(D + a.desc_off), lane};
-                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768 | 131072 | 524288))>(D, n, T, em, lane);
+                c = lz4_encode_block<WIDE, kReadback, (VAR & (8 | 512 | 2048 | 16384 | 32768 | 131072 | 524288)) |
+                                                          (EK == 4 ? kOptCountFirst : 0)>(D, n, T, em, lane);
                 KSTAMP(1);
                 if (em.ns > kDescMax) c = -1;  // more sequences than descriptor slots
                 if (c >= 0) {
