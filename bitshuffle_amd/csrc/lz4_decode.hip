@@ -72,8 +72,11 @@ struct DDiag {
 };
 #endif
 
+// global, not generic, byte loads: a flat load also counts on lgkmcnt (an LDS
+// wait then waits for it too) and reads as divergent to the compiler
 __device__ __forceinline__ uint32_t be32_global(const uint8_t* p) {
-    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+    const gbl8c* q = (const gbl8c*)p;
+    return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
 }
 
 // Follow the chain from p until it reaches/passes `stop` or Cb; returns the
@@ -1091,8 +1094,77 @@ struct SeqOutLane0 {
     }
 };
 
+// BSHUF_SCAN_BIG_LDS=0 (default): the window lives in registers instead --
+// 1 KiB of the record in four VGPRs (lane l, dword d: bytes 4l + 256d) plus the
+// next 1 KiB already in flight -- and a byte is one v_readlane of a uniform
+// lane, so the whole walk runs on the scalar unit without an LDS round trip per
+// byte, and with no LDS the wave count per CU is not capped by the window.
+#ifndef BSHUF_SCAN_BIG_LDS
+#define BSHUF_SCAN_BIG_LDS 1
+#endif
+#ifndef BSHUF_SCAN_BIG_PF  // 1: the next 1 KiB loaded ahead into four more VGPRs
+#define BSHUF_SCAN_BIG_PF 0
+#endif
+struct RegWin {
+    uint32_t d0, d1, d2, d3;
+};
+struct WaveRegReader {
+    const uint8_t* P;
+    int clen;
+    int w0;  // record position of window byte 0 (P + w0 is 4-byte aligned)
+    int lane;
+    RegWin cur, nxt;
+    // dwords wholly past the record read as 0; one that holds a record byte
+    // never crosses a page (aligned), and bytes before P are the header's
+    __device__ __forceinline__ RegWin load(int base) const {
+        RegWin r{0u, 0u, 0u, 0u};
+        const int b = base + 4 * lane;
+        const gbl32c* q = (const gbl32c*)(P + b);
+        if (b < clen) r.d0 = q[0];
+        if (b + 256 < clen) r.d1 = q[64];
+        if (b + 512 < clen) r.d2 = q[128];
+        if (b + 768 < clen) r.d3 = q[192];
+        return r;
+    }
+    __device__ __forceinline__ uint32_t operator()(int p) {
+        int rel = p - w0;
+        if ((unsigned)rel >= 1024u) {
+#if BSHUF_SCAN_BIG_PF
+            if ((unsigned)(rel - 1024) < 1024u) {
+                cur = nxt;
+                w0 += 1024;
+            } else {
+                w0 = p - (int)((uintptr_t)(P + p) & 3);
+                cur = load(w0);
+            }
+            nxt = load(w0 + 1024);
+#else
+            w0 = p - (int)((uintptr_t)(P + p) & 3);
+            cur = load(w0);
+#endif
+            // wait for the window here, once: redefined by the asm, its
+            // registers are no longer pending loads at the reads below (which
+            // would otherwise each wait for every load and store in flight)
+            asm volatile("" : "+v"(cur.d0), "+v"(cur.d1), "+v"(cur.d2), "+v"(cur.d3));
+            rel = p - w0;
+        }
+        const int d = rel >> 8;
+        // scalar selects of four readlanes: a vector select of the fields
+        // would become a variable index into the reader (kept in memory then)
+        const int li = (rel >> 2) & 63;
+        const uint32_t x0 = (uint32_t)__builtin_amdgcn_readlane((int)cur.d0, li);
+        const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)cur.d1, li);
+        const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)cur.d2, li);
+        const uint32_t x3 = (uint32_t)__builtin_amdgcn_readlane((int)cur.d3, li);
+        const uint32_t x = d == 0 ? x0 : (d == 1 ? x1 : (d == 2 ? x2 : x3));
+        return (x >> (8 * (rel & 3))) & 255u;
+    }
+};
+
 __global__ __launch_bounds__(64) void k_seq_scan_big(DecArgs a, int64_t nb) {
+#if BSHUF_SCAN_BIG_LDS
     __shared__ __attribute__((aligned(16))) uint8_t win[kScanWin];
+#endif
     const int lane = threadIdx.x;
     const int64_t k = blockIdx.x;
     resolve_len(a);
@@ -1102,11 +1174,23 @@ __global__ __launch_bounds__(64) void k_seq_scan_big(DecArgs a, int64_t nb) {
     int64_t o1 = !loc.last ? (int64_t)a.offs[k + 1] : o0 + 4 + (int64_t)a.maxlen;
     clamp_span(o0, o1, loc.in_nbytes, a.maxlen);
     const int64_t avail = o1 - o0;
-    const int64_t clen = avail >= 4 ? (int64_t)(int32_t)be32_global(loc.in + o0) : 0;
+    // the same for every lane (a divergent clen would take the whole walk onto
+    // the vector unit with exec masks)
+    const int64_t clen =
+        avail >= 4 ? (int64_t)__builtin_amdgcn_readfirstlane((int)be32_global(loc.in + o0)) : 0;
     int64_t st = header_status(clen, avail, loc.last, a.maxlen);
     if (st == 0) {
         int cnt = 0;
+#if BSHUF_SCAN_BIG_LDS
         WaveReader rd{loc.in + o0 + 4, (int)clen, -(1 << 30), to_lds(win), lane};
+#else
+        WaveRegReader rd;
+        rd.P = loc.in + o0 + 4;
+        rd.clen = (int)clen;
+        rd.w0 = -(1 << 30);
+        rd.lane = lane;
+        rd.cur = rd.nxt = RegWin{0u, 0u, 0u, 0u};
+#endif
         SeqOutLane0 out;
         out.lane = lane;
         out.o.base = loc.seq + o0 / 3;
